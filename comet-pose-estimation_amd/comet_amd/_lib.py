@@ -1,0 +1,98 @@
+"""ctypes binding of libcomet_hip.so (include/comet_hip.h).
+
+The product path has no fallback: if the library is missing or fails to load, every op raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("COMET_HIP_LIB", os.path.join(os.path.dirname(_HERE), "libcomet_hip.so"))
+
+F32 = 0
+BF16 = 1
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_SIGMOID = 0, 1, 2, 3
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_vp = ctypes.c_void_p
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype_ab", c_i32), ("dtype_c", c_i32), ("layout_a", c_i32), ("layout_b", c_i32),
+        ("m", c_i64), ("n", c_i64), ("k", c_i64), ("batch", c_i64 * 2),
+        ("a", c_vp), ("lda", c_i64), ("stride_a", c_i64 * 2),
+        ("b", c_vp), ("ldb", c_i64), ("stride_b", c_i64 * 2),
+        ("c", c_vp), ("ldc", c_i64), ("stride_c", c_i64 * 2),
+        ("bias", c_vp), ("bias_mode", c_i32), ("stride_bias", c_i64 * 2),
+        ("resid", c_vp), ("ldr", c_i64), ("stride_r", c_i64 * 2),
+        ("aux", c_vp), ("ldaux", c_i64), ("stride_aux", c_i64 * 2),
+        ("alpha", ctypes.c_float), ("beta", ctypes.c_float), ("act", c_i32),
+    ]
+
+
+class AttnArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", c_i32), ("head_dim", c_i32),
+        ("batch", c_i64), ("heads", c_i64), ("lq", c_i64), ("lk", c_i64),
+        ("q", c_vp), ("sq_b", c_i64), ("sq_h", c_i64), ("sq_l", c_i64),
+        ("k", c_vp), ("sk_b", c_i64), ("sk_h", c_i64), ("sk_l", c_i64),
+        ("v", c_vp), ("sv_b", c_i64), ("sv_h", c_i64), ("sv_l", c_i64),
+        ("o", c_vp), ("so_b", c_i64), ("so_h", c_i64), ("so_l", c_i64),
+        ("lse", c_vp), ("scale", ctypes.c_float),
+    ]
+
+
+# (name, restype, argtypes); every exported symbol of include/comet_hip.h
+_F = ctypes.c_float
+_INT = ctypes.c_int
+SIGNATURES = {
+    "comet_version": (_INT, []),
+    "comet_last_error": (ctypes.c_char_p, []),
+    "comet_gemm": (_INT, [ctypes.POINTER(GemmArgs), c_vp]),
+    "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, _F, c_vp]),
+    "comet_layernorm_bwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, _INT, c_vp]),
+    "comet_attention_fwd": (_INT, [ctypes.POINTER(AttnArgs), c_vp]),
+    "comet_attn_probs": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _F, c_vp]),
+    "comet_attn_delta": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "comet_attn_dsoftmax": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, _F, c_vp]),
+    "comet_cast": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_vp]),
+    "comet_act_bwd": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_vp, _INT, c_i64, c_vp]),
+    "comet_axpby": (_INT, [c_vp, c_vp, _F, _F, c_i64, c_vp]),
+    "comet_colsum": (_INT, [_INT, c_vp, c_vp, c_i64, c_i64, c_i64, _INT, c_vp]),
+    "comet_sq_norm_multi": (_INT, [c_vp, c_vp, _INT, c_vp, c_vp]),
+    "comet_adamw_multi": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, _INT, _F, _F, _F, _F, _F, _INT, c_vp, _F, c_vp]),
+    "comet_im2col_nhwc": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _INT, _INT, _INT, _INT, c_i64, c_i64, c_i64, c_vp]),
+    "comet_instnorm_nhwc": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, _F, _INT, _INT, c_vp]),
+    "comet_resize_bilinear": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, _INT, c_vp]),
+}
+
+_lib = None
+
+
+class CometHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libcomet_hip.so once; raise (never fall back) if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise CometHipError(
+            f"libcomet_hip.so not found at {LIB_PATH}: build it with `make -C comet-pose-estimation_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().comet_last_error()
+        raise CometHipError(f"{what}: {msg.decode() if msg else 'error'} (code {rc})")

@@ -1,0 +1,379 @@
+// Fused multi-head attention forward + materialised-backward helpers.
+//
+// Replaces nn.MultiheadAttention's explicit q·kᵀ·scale → softmax → ·v path (SURVEY Appendix
+// B-17; modules.py:290,339) at every use site of the hot path: head self/cross attention
+// (camera_predictor10.py:663-683), T_P cross attention (329-348), trunk (382), tracker time /
+// space blocks (blocks.py:312-340) and the DINOv2 backbone.
+//
+// Forward structure (one workgroup = 4 waves = 64 queries of one (batch, head)):
+//  * each wave owns 16 queries, Q fragments live in registers for the whole kernel;
+//  * K/V tiles of 64 keys are staged global -> registers -> LDS (next tile's global loads are
+//    issued before the current tile's MFMAs);
+//  * Sᵀ = K·Qᵀ is computed ("swapped" product): the accumulator has the query on the lane and
+//    the keys in registers, so the running max / sum of a query are lane-local plus two
+//    shuffles over the four 16-lane groups;
+//  * Oᵀ = Vᵀ·Pᵀ takes P straight from the Sᵀ registers as the B operand (k order permuted
+//    consistently for both operands); the Vᵀ fragments come from a row-major V tile via
+//    ds_read_b64_tr_b16 (bf16) or plain ds_read_b32 (f32).
+#include "common.hpp"
+
+namespace comet {
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+template <typename T, int D> struct ACfg;
+template <int D> struct ACfg<__bf16, D> {
+  static constexpr int DA = ((D + 31) / 32) * 32;  // k-dim of the Q·Kᵀ MFMA (x32)
+  static constexpr int KP = DA + 8;                 // LDS row pitch (elements)
+  static constexpr int VEC = 8;
+};
+template <int D> struct ACfg<float, D> {
+  static constexpr int DA = ((D + 15) / 16) * 16;
+  static constexpr int KP = DA + 4;
+  static constexpr int VEC = 4;
+};
+
+template <typename T> struct AVec;
+template <> struct AVec<__bf16> { typedef uint4 type; };
+template <> struct AVec<float> { typedef float4 type; };
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <typename T, int D>
+__global__ void __launch_bounds__(256)
+attn_fwd_kernel(const T* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_l,
+                const T* __restrict__ K, int64_t sk_b, int64_t sk_h, int64_t sk_l,
+                const T* __restrict__ V, int64_t sv_b, int64_t sv_h, int64_t sv_l,
+                T* __restrict__ O, int64_t so_b, int64_t so_h, int64_t so_l,
+                float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2) {
+  typedef ACfg<T, D> C;
+  constexpr int DA = C::DA, KP = C::KP, VEC = C::VEC;
+  constexpr int DT = (D + 15) / 16;
+  constexpr bool BF = sizeof(T) == 2;
+  constexpr int NVROW = D / VEC;                    // vectors per key row
+  constexpr int NVT = (64 * NVROW + 255) / 256;     // vectors per thread per tile
+  typedef typename AVec<T>::type vec_t;
+
+  __shared__ __attribute__((aligned(16))) T Ks[64 * KP];
+  __shared__ __attribute__((aligned(16))) T Vs[64 * KP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 15, hg = lane >> 4;
+  const int64_t bh = blockIdx.y;
+  const int64_t b = bh / heads, h = bh % heads;
+  Q += b * sq_b + h * sq_h;
+  K += b * sk_b + h * sk_h;
+  V += b * sv_b + h * sv_h;
+  O += b * so_b + h * so_h;
+
+  // zero LDS once: pad columns [D, DA) stay zero for the whole kernel
+  for (int i = tid; i < 64 * KP; i += 256) { Ks[i] = T(0.f); Vs[i] = T(0.f); }
+
+  // ---- Q fragments (registers) ----
+  const int q = blockIdx.x * 64 + wid * 16 + li;
+  const bool qok = q < lq;
+  constexpr int NQC = BF ? DA / 32 : DA / 16;
+  typedef typename std::conditional<BF, bf16x8, f32x4>::type qfrag_t;
+  qfrag_t qf[NQC];
+#pragma unroll
+  for (int c = 0; c < NQC; ++c) {
+    const int d0 = BF ? 32 * c + 8 * hg : 16 * c + 4 * hg;
+    if (qok && d0 < D) {
+      qf[c] = *reinterpret_cast<const qfrag_t*>(Q + (int64_t)q * sq_l + d0);
+    } else {
+      qf[c] = qfrag_t{};
+    }
+  }
+
+  f32x4 o[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int ntiles = (lk + 63) / 64;
+  vec_t kreg[NVT], vreg[NVT];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NVT; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / NVROW, cv = (idx % NVROW) * VEC;
+      const int key = t * 64 + row;
+      if (idx < 64 * NVROW && key < lk) {
+        kreg[i] = *reinterpret_cast<const vec_t*>(K + (int64_t)key * sk_l + cv);
+        vreg[i] = *reinterpret_cast<const vec_t*>(V + (int64_t)key * sv_l + cv);
+      } else {
+        kreg[i] = vec_t{};
+        vreg[i] = vec_t{};
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < NVT; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < 64 * NVROW) {
+        const int row = idx / NVROW, cv = (idx % NVROW) * VEC;
+        *reinterpret_cast<vec_t*>(Ks + row * KP + cv) = kreg[i];
+        *reinterpret_cast<vec_t*>(Vs + row * KP + cv) = vreg[i];
+      }
+    }
+  };
+
+  gload(0);
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();  // previous tile fully consumed (and LDS zeroing done)
+    lstore();
+    __syncthreads();
+    if (t + 1 < ntiles) gload(t + 1);
+
+    // ---- Sᵀ = K·Qᵀ : 4 subtiles of 16 keys ----
+    f32x4 s[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      s[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const T* krow = Ks + (st * 16 + li) * KP;
+      if constexpr (BF) {
+#pragma unroll
+        for (int c = 0; c < NQC; ++c) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 32 * c + 8 * hg);
+          s[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[c], s[st], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < NQC; ++c) {
+          const f32x4 kf = *reinterpret_cast<const f32x4*>(krow + 16 * c + 4 * hg);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            s[st] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[e], qf[c][e], s[st], 0, 0, 0);
+        }
+      }
+    }
+    // ---- online softmax (log2 domain); key of s[st][r] = t*64 + st*16 + 4*hg + r ----
+    float mt = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = t * 64 + st * 16 + 4 * hg + r;
+        const float v = key < lk ? s[st][r] * scale_log2 : -INFINITY;
+        s[st][r] = v;
+        mt = fmaxf(mt, v);
+      }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = exp2f(m_run - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[st][r] - m_new);
+        s[st][r] = p;
+        ls += p;
+      }
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < DT; ++i) o[i] *= alpha;
+
+    // ---- Oᵀ += Vᵀ·Pᵀ ----
+    if constexpr (BF) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x4 p0 = __builtin_convertvector(s[2 * u], bf16x4);
+        const bf16x4 p1 = __builtin_convertvector(s[2 * u + 1], bf16x4);
+        const bf16x8 pf = __builtin_shufflevector(p0, p1, 0, 1, 2, 3, 4, 5, 6, 7);
+        const int qq = li >> 2, pp = li & 3;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const T* a0 = Vs + (16 * (2 * u) + 4 * hg + qq) * KP + 16 * dt + 4 * pp;
+          const T* a1 = Vs + (16 * (2 * u + 1) + 4 * hg + qq) * KP + 16 * dt + 4 * pp;
+          const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+          const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[dt], 0, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const T* vrow = Vs + (16 * st + 4 * hg + r) * KP + li;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vrow[16 * dt], s[st][r], o[dt], 0, 0, 0);
+        }
+    }
+  }
+
+  // ---- epilogue ----
+  float l_tot = l_run;
+  l_tot += __shfl_xor(l_tot, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  if (!qok) return;
+  const float inv = 1.f / l_tot;
+  T* orow = O + (int64_t)q * so_l;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int d0 = 16 * dt + 4 * hg;
+    if (d0 < D) {
+      if constexpr (BF) {
+        bf16x4 w;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w[r] = static_cast<__bf16>(o[dt][r] * inv);
+        *reinterpret_cast<bf16x4*>(orow + d0) = w;
+      } else {
+        f32x4 w = o[dt] * inv;
+        *reinterpret_cast<f32x4*>(orow + d0) = w;
+      }
+    }
+  }
+  if (LSE && hg == 0) LSE[bh * lq + q] = (m_run + log2f(l_tot)) * LN2;
+}
+
+template <typename T, int D>
+int launch_fwd(const comet_attn_args& a, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(a.lq, 64), (unsigned)(a.batch * a.heads));
+  hipLaunchKernelGGL((attn_fwd_kernel<T, D>), grid, dim3(256), 0, s,
+                     (const T*)a.q, a.sq_b, a.sq_h, a.sq_l, (const T*)a.k, a.sk_b, a.sk_h, a.sk_l,
+                     (const T*)a.v, a.sv_b, a.sv_h, a.sv_l, (T*)a.o, a.so_b, a.so_h, a.so_l,
+                     a.lse, (int)a.heads, (int)a.lq, (int)a.lk, a.scale * LOG2E);
+  COMET_CHECK_LAUNCH("comet_attention_fwd");
+  return COMET_OK;
+}
+
+template <typename T>
+int dispatch_d(const comet_attn_args& a, hipStream_t s) {
+  switch (a.head_dim) {
+    case 32: return launch_fwd<T, 32>(a, s);
+    case 48: return launch_fwd<T, 48>(a, s);
+    case 64: return launch_fwd<T, 64>(a, s);
+    case 96: return launch_fwd<T, 96>(a, s);
+    default: set_error("comet_attention_fwd: head_dim must be 32, 48, 64 or 96"); return COMET_EINVAL;
+  }
+}
+
+// ---- materialised backward helpers ----
+template <typename T>
+__global__ void probs_kernel(const T* __restrict__ S, const float* __restrict__ lse,
+                             T* __restrict__ P, int64_t rows, int64_t cols, int64_t lds,
+                             int64_t ldp, float scale) {
+  const int64_t r = blockIdx.y * (int64_t)gridDim.z + blockIdx.z;
+  if (r >= rows) return;
+  const float l = lse[r];
+  for (int64_t c = blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256)
+    P[r * ldp + c] = from_f32<T>(__expf(to_f32(S[r * lds + c]) * scale - l));
+}
+
+template <typename T>
+__global__ void delta_kernel(const T* __restrict__ dO, const T* __restrict__ Out,
+                             float* __restrict__ delta, int64_t heads, int64_t lq, int64_t d,
+                             int64_t so_b, int64_t so_h, int64_t so_l, int64_t sd_b,
+                             int64_t sd_h, int64_t sd_l, int64_t rows) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t bh = r / lq, qi = r % lq, b = bh / heads, h = bh % heads;
+  const T* o = Out + b * so_b + h * so_h + qi * so_l;
+  const T* g = dO + b * sd_b + h * sd_h + qi * sd_l;
+  float acc = 0.f;
+  for (int64_t i = lane; i < d; i += 64) acc += to_f32(o[i]) * to_f32(g[i]);
+  acc = wave_sum(acc);
+  if (lane == 0) delta[r] = acc;
+}
+
+template <typename T>
+__global__ void dsoftmax_kernel(const T* __restrict__ P, const T* __restrict__ dP,
+                                const float* __restrict__ delta, T* __restrict__ dS,
+                                int64_t rows, int64_t cols, int64_t ld, float scale) {
+  const int64_t r = blockIdx.y * (int64_t)gridDim.z + blockIdx.z;
+  if (r >= rows) return;
+  const float dl = delta[r];
+  for (int64_t c = blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256) {
+    const int64_t i = r * ld + c;
+    dS[i] = from_f32<T>(to_f32(P[i]) * (to_f32(dP[i]) - dl) * scale);
+  }
+}
+
+inline dim3 row_grid(int64_t rows, int64_t cols) {
+  const unsigned gx = (unsigned)(cdiv(cols, 256) < 4 ? cdiv(cols, 256) : 4);
+  // rows split over y*z to stay under the 65535 limit
+  int64_t gz = rows < 65535 ? rows : 65535;
+  int64_t gy = cdiv(rows, gz);
+  return dim3(gx, (unsigned)gy, (unsigned)gz);
+}
+
+}  // namespace
+}  // namespace comet
+
+using namespace comet;
+
+extern "C" int comet_attention_fwd(const comet_attn_args* args, void* stream) {
+  COMET_CHECK_ARG(args != nullptr, "comet_attention_fwd: null args");
+  const comet_attn_args& a = *args;
+  COMET_CHECK_ARG(a.q && a.k && a.v && a.o, "comet_attention_fwd: null tensor");
+  COMET_CHECK_ARG(a.batch > 0 && a.heads > 0 && a.lq >= 0 && a.lk > 0, "comet_attention_fwd: bad sizes");
+  COMET_CHECK_ARG(a.batch * a.heads <= 65535, "comet_attention_fwd: batch*heads > 65535");
+  const int vec = a.dtype == COMET_BF16 ? 8 : 4;
+  const int64_t strides[] = {a.sq_b, a.sq_h, a.sq_l, a.sk_b, a.sk_h, a.sk_l,
+                             a.sv_b, a.sv_h, a.sv_l, a.so_b, a.so_h, a.so_l};
+  for (int64_t st : strides) COMET_CHECK_ARG(st % vec == 0, "comet_attention_fwd: strides must be multiples of 16 bytes");
+  COMET_CHECK_ARG(((uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v | (uintptr_t)a.o) % 16 == 0,
+                  "comet_attention_fwd: tensors must be 16-byte aligned");
+  if (a.lq == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  if (a.dtype == COMET_BF16) return dispatch_d<__bf16>(a, s);
+  if (a.dtype == COMET_F32) return dispatch_d<float>(a, s);
+  set_error("comet_attention_fwd: bad dtype");
+  return COMET_EINVAL;
+}
+
+extern "C" int comet_attn_probs(int dtype_s, const void* s, const float* lse, void* p, int64_t rows,
+                                int64_t cols, int64_t ld_s, int64_t ld_p, float scale, void* stream) {
+  COMET_CHECK_ARG(s && lse && p, "comet_attn_probs: null pointer");
+  if (rows == 0 || cols == 0) return COMET_OK;
+  hipStream_t st = as_stream(stream);
+  dim3 g = row_grid(rows, cols);
+  if (dtype_s == COMET_F32)
+    hipLaunchKernelGGL((probs_kernel<float>), g, dim3(256), 0, st, (const float*)s, lse, (float*)p, rows, cols, ld_s, ld_p, scale);
+  else
+    hipLaunchKernelGGL((probs_kernel<__bf16>), g, dim3(256), 0, st, (const __bf16*)s, lse, (__bf16*)p, rows, cols, ld_s, ld_p, scale);
+  COMET_CHECK_LAUNCH("comet_attn_probs");
+  return COMET_OK;
+}
+
+extern "C" int comet_attn_delta(int dtype, const void* dout, const void* out, float* delta,
+                                int64_t batch, int64_t heads, int64_t lq, int64_t d, int64_t so_b,
+                                int64_t so_h, int64_t so_l, int64_t sdo_b, int64_t sdo_h,
+                                int64_t sdo_l, void* stream) {
+  COMET_CHECK_ARG(dout && out && delta, "comet_attn_delta: null pointer");
+  const int64_t rows = batch * heads * lq;
+  if (rows == 0) return COMET_OK;
+  hipStream_t st = as_stream(stream);
+  dim3 g((unsigned)cdiv(rows, 4));
+  if (dtype == COMET_F32)
+    hipLaunchKernelGGL((delta_kernel<float>), g, dim3(256), 0, st, (const float*)dout, (const float*)out, delta, heads, lq, d, so_b, so_h, so_l, sdo_b, sdo_h, sdo_l, rows);
+  else
+    hipLaunchKernelGGL((delta_kernel<__bf16>), g, dim3(256), 0, st, (const __bf16*)dout, (const __bf16*)out, delta, heads, lq, d, so_b, so_h, so_l, sdo_b, sdo_h, sdo_l, rows);
+  COMET_CHECK_LAUNCH("comet_attn_delta");
+  return COMET_OK;
+}
+
+extern "C" int comet_attn_dsoftmax(int dtype_p, const void* p, const void* dp, const float* delta,
+                                   void* ds, int64_t rows, int64_t cols, int64_t ld, float scale,
+                                   void* stream) {
+  COMET_CHECK_ARG(p && dp && delta && ds, "comet_attn_dsoftmax: null pointer");
+  if (rows == 0 || cols == 0) return COMET_OK;
+  hipStream_t st = as_stream(stream);
+  dim3 g = row_grid(rows, cols);
+  if (dtype_p == COMET_F32)
+    hipLaunchKernelGGL((dsoftmax_kernel<float>), g, dim3(256), 0, st, (const float*)p, (const float*)dp, delta, (float*)ds, rows, cols, ld, scale);
+  else
+    hipLaunchKernelGGL((dsoftmax_kernel<__bf16>), g, dim3(256), 0, st, (const __bf16*)p, (const __bf16*)dp, delta, (__bf16*)ds, rows, cols, ld, scale);
+  COMET_CHECK_LAUNCH("comet_attn_dsoftmax");
+  return COMET_OK;
+}

@@ -1,0 +1,108 @@
+// CNN operators on channels-last activations: im2col for the tracker encoders / DINOv2
+// patch-embed convolutions, and align_corners=True bilinear resize.
+//
+// Reference sites: blocks.py:27-111 (BasicEncoder: conv7x7 s2, 3x3, 1x1, bilinear
+// up-sampling), blocks.py:114-202 (ShallowEncoder on 31x31 patches), modules.py:39-116
+// (ResidualBlock), track_predictor.py:137-143 (x1/2 resize), camera_predictor10.py:624-630
+// (512 -> 336 resize), DINOv2 patch_embed (conv 14x14 s14).
+#include "common.hpp"
+
+namespace comet {
+namespace {
+
+// cols[(n*oh + oy)*ow + ox][(ky*kw + kx)*c + ci] = x[n][oy*s - p + ky][ox*s - p + kx][ci]
+template <typename TI, typename TO>
+__global__ void im2col_nhwc_kernel(const TI* __restrict__ x, TO* __restrict__ cols, int64_t n,
+                                   int64_t h, int64_t w, int64_t c, int kh, int kw, int stride,
+                                   int pad, int64_t oh, int64_t ow, int64_t ldc) {
+  const int64_t kk = (int64_t)kh * kw * c;
+  const int64_t total = n * oh * ow * kk;
+  const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gs) {
+    const int64_t col = i % kk, pix = i / kk;
+    const int64_t ci = col % c, kx = (col / c) % kw, ky = col / (c * kw);
+    const int64_t ox = pix % ow, oy = (pix / ow) % oh, ni = pix / (ow * oh);
+    const int64_t iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+    float v = 0.f;
+    if (iy >= 0 && iy < h && ix >= 0 && ix < w) v = to_f32(x[((ni * h + iy) * w + ix) * c + ci]);
+    cols[pix * ldc + col] = from_f32<TO>(v);
+  }
+}
+
+// align_corners=True bilinear: src = dst * (in-1)/(out-1)
+__device__ __forceinline__ void ac_coord(int64_t o, int64_t in, int64_t out, int64_t& i0,
+                                         int64_t& i1, float& f) {
+  const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+  const float src = scale * (float)o;
+  i0 = (int64_t)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + 1 < in ? i0 + 1 : in - 1;
+  f = src - (float)i0;
+}
+
+template <typename TI, typename TO>
+__global__ void resize_kernel(const TI* __restrict__ x, TO* __restrict__ y, int nhwc, int64_t n,
+                              int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow, int add) {
+  const int64_t total = n * c * oh * ow;
+  const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gs) {
+    int64_t ni, ci, oy, ox;
+    if (nhwc) { ci = i % c; ox = (i / c) % ow; oy = (i / (c * ow)) % oh; ni = i / (c * ow * oh); }
+    else { ox = i % ow; oy = (i / ow) % oh; ci = (i / (ow * oh)) % c; ni = i / (ow * oh * c); }
+    int64_t y0, y1, x0, x1; float fy, fx;
+    ac_coord(oy, h, oh, y0, y1, fy);
+    ac_coord(ox, w, ow, x0, x1, fx);
+    auto at = [&](int64_t yy, int64_t xx) -> float {
+      return nhwc ? to_f32(x[((ni * h + yy) * w + xx) * c + ci])
+                  : to_f32(x[((ni * c + ci) * h + yy) * w + xx]);
+    };
+    const float v00 = at(y0, x0), v01 = at(y0, x1), v10 = at(y1, x0), v11 = at(y1, x1);
+    // same association as ATen's upsample_bilinear2d: h0lambda*(w0l*v00 + w1l*v01) + h1lambda*(...)
+    const float v = (1.f - fy) * ((1.f - fx) * v00 + fx * v01) + fy * ((1.f - fx) * v10 + fx * v11);
+    float out = v;
+    if (add) out += to_f32(y[i]);
+    y[i] = from_f32<TO>(out);
+  }
+}
+
+inline unsigned g1d(int64_t n) {
+  int64_t g = cdiv(n, 256);
+  return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+}  // namespace comet
+
+using namespace comet;
+
+extern "C" int comet_im2col_nhwc(int dtype_in, int dtype_out, const void* x, void* cols, int64_t n,
+                                 int64_t h, int64_t w, int64_t c, int kh, int kw, int stride,
+                                 int pad, int64_t oh, int64_t ow, int64_t ldc, void* stream) {
+  COMET_CHECK_ARG(x && cols && n > 0 && c > 0 && kh > 0 && kw > 0 && stride > 0, "comet_im2col_nhwc: bad args");
+  hipStream_t s = as_stream(stream);
+  const unsigned g = g1d(n * oh * ow * kh * kw * c);
+#define IC(TI, TO) hipLaunchKernelGGL((im2col_nhwc_kernel<TI, TO>), dim3(g), dim3(256), 0, s, (const TI*)x, (TO*)cols, n, h, w, c, kh, kw, stride, pad, oh, ow, ldc)
+  if (dtype_in == COMET_F32 && dtype_out == COMET_F32) IC(float, float);
+  else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) IC(float, __bf16);
+  else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) IC(__bf16, __bf16);
+  else IC(__bf16, float);
+#undef IC
+  COMET_CHECK_LAUNCH("comet_im2col_nhwc");
+  return COMET_OK;
+}
+
+extern "C" int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, const void* x, void* y,
+                                     int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh,
+                                     int64_t ow, int add, void* stream) {
+  COMET_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "comet_resize_bilinear: bad args");
+  hipStream_t s = as_stream(stream);
+  const unsigned g = g1d(n * c * oh * ow);
+#define RS(TI, TO) hipLaunchKernelGGL((resize_kernel<TI, TO>), dim3(g), dim3(256), 0, s, (const TI*)x, (TO*)y, nhwc, n, c, h, w, oh, ow, add)
+  if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RS(float, float);
+  else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) RS(float, __bf16);
+  else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) RS(__bf16, __bf16);
+  else RS(__bf16, float);
+#undef RS
+  COMET_CHECK_LAUNCH("comet_resize_bilinear");
+  return COMET_OK;
+}

@@ -1,0 +1,228 @@
+// Elementwise, reduction and optimizer kernels: dtype cast, activation backward, axpby,
+// column sums (bias grads), multi-tensor squared norm (clip_grad_norm_) and fused AdamW.
+//
+// Reference sites: train_eval_func_new_cp5.py:790-801 (backward, clip_grad_norm_(1.0),
+// optimizer.step), train_util.py:311-332 (AdamW over camera_predictor.parameters()).
+#include "common.hpp"
+
+namespace comet {
+namespace {
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = from_f32<TO>(to_f32(x[i]));
+}
+
+template <typename TP, typename TD, typename TX>
+__global__ void act_bwd_kernel(int act, const TP* __restrict__ pre, const TD* __restrict__ dy,
+                               TX* __restrict__ dx, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float p = to_f32(pre[i]), d = to_f32(dy[i]);
+    float g;
+    switch (act) {
+      case COMET_ACT_GELU: g = gelu_erf_grad(p); break;
+      case COMET_ACT_RELU: g = p > 0.f ? 1.f : 0.f; break;
+      case COMET_ACT_SIGMOID: { const float s = 1.f / (1.f + __expf(-p)); g = s * (1.f - s); break; }
+      default: g = 1.f;
+    }
+    dx[i] = from_f32<TX>(d * g);
+  }
+}
+
+__global__ void axpby_kernel(const float* __restrict__ x, float* __restrict__ y, float a, float b,
+                             int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = a * x[i] + b * y[i];
+}
+
+// out[c] (+)= sum_r x[r*ld + c]; block = 256 columns x ROWCHUNK rows, atomics per block.
+constexpr int COLSUM_ROWS = 1024;
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ x, float* __restrict__ out, int64_t rows,
+                              int64_t cols, int64_t ld) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS;
+  const int64_t r1 = r0 + COLSUM_ROWS < rows ? r0 + COLSUM_ROWS : rows;
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += to_f32(x[r * ld + c]);
+  atomicAdd(out + c, s);
+}
+
+constexpr int MT_MAX = 24;
+struct MultiPtr {
+  float* p[MT_MAX];
+  const float* g[MT_MAX];
+  float* m[MT_MAX];
+  float* v[MT_MAX];
+  int64_t n[MT_MAX];
+  int count;
+};
+
+__global__ void sq_norm_kernel(MultiPtr mp, float* __restrict__ out) {
+  __shared__ float scratch[4];
+  float s = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int t = 0; t < mp.count; ++t) {
+    const float* x = mp.g[t];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mp.n[t]; i += stride) {
+      const float v = x[i];
+      s += v * v;
+    }
+  }
+  s = block_sum<4>(s, scratch);
+  if (threadIdx.x == 0) atomicAdd(out, s);
+}
+
+// torch.optim.AdamW (foreach=False semantics): p *= 1 - lr*wd; m.lerp_(g, 1-b1);
+// v = b2*v + (1-b2)*g^2; p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps).
+__global__ void adamw_kernel(MultiPtr mp, float lr, float b1, float b2, float eps, float wd,
+                             float bc1, float bc2_sqrt, const float* __restrict__ sqnorm,
+                             float max_norm) {
+  float clip = 1.f;
+  if (sqnorm) {
+    const float total = sqrtf(*sqnorm);
+    const float coef = max_norm / (total + 1e-6f);
+    clip = coef < 1.f ? coef : 1.f;
+  }
+  const float step_size = lr / bc1;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int t = 0; t < mp.count; ++t) {
+    float* p = mp.p[t]; const float* g = mp.g[t]; float* m = mp.m[t]; float* v = mp.v[t];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mp.n[t]; i += stride) {
+      const float gi = g[i] * clip;
+      float pi = p[i] * (1.f - lr * wd);
+      float mi = m[i];
+      mi = mi + (1.f - b1) * (gi - mi);
+      const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+      const float denom = sqrtf(vi) / bc2_sqrt + eps;
+      pi = pi - step_size * (mi / denom);
+      p[i] = pi; m[i] = mi; v[i] = vi;
+    }
+  }
+}
+
+inline unsigned grid_for(int64_t n, int bs = 256) {
+  int64_t g = cdiv(n, bs);
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+}  // namespace
+}  // namespace comet
+
+using namespace comet;
+
+extern "C" int comet_cast(int dtype_in, int dtype_out, const void* x, void* y, int64_t n,
+                          void* stream) {
+  COMET_CHECK_ARG(x && y, "comet_cast: null pointer");
+  if (n == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  const unsigned g = grid_for(n);
+  if (dtype_in == COMET_F32 && dtype_out == COMET_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, __bf16>), dim3(g), dim3(256), 0, s, (const float*)x, (__bf16*)y, n);
+  else if (dtype_in == COMET_BF16 && dtype_out == COMET_F32)
+    hipLaunchKernelGGL((cast_kernel<__bf16, float>), dim3(g), dim3(256), 0, s, (const __bf16*)x, (float*)y, n);
+  else if (dtype_in == COMET_F32 && dtype_out == COMET_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(g), dim3(256), 0, s, (const float*)x, (float*)y, n);
+  else
+    hipLaunchKernelGGL((cast_kernel<__bf16, __bf16>), dim3(g), dim3(256), 0, s, (const __bf16*)x, (__bf16*)y, n);
+  COMET_CHECK_LAUNCH("comet_cast");
+  return COMET_OK;
+}
+
+extern "C" int comet_act_bwd(int act, int dtype_pre, int dtype_dy, const void* pre, const void* dy,
+                             void* dx, int dtype_dx, int64_t n, void* stream) {
+  COMET_CHECK_ARG(pre && dy && dx, "comet_act_bwd: null pointer");
+  if (n == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  const unsigned g = grid_for(n);
+#define AB(TP, TD, TX) \
+  hipLaunchKernelGGL((act_bwd_kernel<TP, TD, TX>), dim3(g), dim3(256), 0, s, act, (const TP*)pre, (const TD*)dy, (TX*)dx, n)
+  if (dtype_pre == COMET_F32 && dtype_dy == COMET_F32 && dtype_dx == COMET_F32) AB(float, float, float);
+  else if (dtype_pre == COMET_BF16 && dtype_dy == COMET_F32 && dtype_dx == COMET_BF16) AB(__bf16, float, __bf16);
+  else if (dtype_pre == COMET_BF16 && dtype_dy == COMET_BF16 && dtype_dx == COMET_BF16) AB(__bf16, __bf16, __bf16);
+  else if (dtype_pre == COMET_BF16 && dtype_dy == COMET_F32 && dtype_dx == COMET_F32) AB(__bf16, float, float);
+  else if (dtype_pre == COMET_F32 && dtype_dy == COMET_F32 && dtype_dx == COMET_BF16) AB(float, float, __bf16);
+  else { set_error("comet_act_bwd: unsupported dtype combination"); return COMET_EINVAL; }
+#undef AB
+  COMET_CHECK_LAUNCH("comet_act_bwd");
+  return COMET_OK;
+}
+
+extern "C" int comet_axpby(const float* x, float* y, float a, float b, int64_t n, void* stream) {
+  COMET_CHECK_ARG(x && y, "comet_axpby: null pointer");
+  if (n == 0) return COMET_OK;
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, y, a, b, n);
+  COMET_CHECK_LAUNCH("comet_axpby");
+  return COMET_OK;
+}
+
+extern "C" int comet_colsum(int dtype, const void* x, float* out, int64_t rows, int64_t cols,
+                            int64_t ld, int accumulate, void* stream) {
+  COMET_CHECK_ARG(x && out && cols > 0, "comet_colsum: bad args");
+  hipStream_t s = as_stream(stream);
+  if (!accumulate) {
+    hipError_t e = hipMemsetAsync(out, 0, cols * sizeof(float), s);
+    if (e != hipSuccess) { set_error("comet_colsum: memset failed"); return COMET_ELAUNCH; }
+  }
+  if (rows == 0) return COMET_OK;
+  COMET_CHECK_ARG(cdiv(rows, COLSUM_ROWS) <= 65535, "comet_colsum: too many rows");
+  dim3 grid((unsigned)cdiv(cols, 256), (unsigned)cdiv(rows, COLSUM_ROWS));
+  if (dtype == COMET_F32)
+    hipLaunchKernelGGL((colsum_kernel<float>), grid, dim3(256), 0, s, (const float*)x, out, rows, cols, ld);
+  else
+    hipLaunchKernelGGL((colsum_kernel<__bf16>), grid, dim3(256), 0, s, (const __bf16*)x, out, rows, cols, ld);
+  COMET_CHECK_LAUNCH("comet_colsum");
+  return COMET_OK;
+}
+
+extern "C" int comet_sq_norm_multi(const float* const* ptrs, const int64_t* sizes, int n_tensors,
+                                   float* out, void* stream) {
+  COMET_CHECK_ARG(out && n_tensors >= 0, "comet_sq_norm_multi: bad args");
+  hipStream_t s = as_stream(stream);
+  for (int base = 0; base < n_tensors; base += MT_MAX) {
+    MultiPtr mp{};
+    mp.count = n_tensors - base < MT_MAX ? n_tensors - base : MT_MAX;
+    int64_t total = 0;
+    for (int i = 0; i < mp.count; ++i) {
+      mp.g[i] = ptrs[base + i];
+      mp.n[i] = sizes[base + i];
+      total += mp.n[i];
+    }
+    hipLaunchKernelGGL(sq_norm_kernel, dim3(grid_for(total / 4 + 1)), dim3(256), 0, s, mp, out);
+    COMET_CHECK_LAUNCH("comet_sq_norm_multi");
+  }
+  return COMET_OK;
+}
+
+extern "C" int comet_adamw_multi(float* const* params, const float* const* grads,
+                                 float* const* exp_avg, float* const* exp_avg_sq,
+                                 const int64_t* sizes, int n_tensors, float lr, float beta1,
+                                 float beta2, float eps, float weight_decay, int step,
+                                 const float* sqnorm, float max_norm, void* stream) {
+  COMET_CHECK_ARG(step >= 1, "comet_adamw_multi: step must be >= 1");
+  hipStream_t s = as_stream(stream);
+  const float bc1 = 1.f - powf(beta1, (float)step);
+  const float bc2_sqrt = sqrtf(1.f - powf(beta2, (float)step));
+  for (int base = 0; base < n_tensors; base += MT_MAX) {
+    MultiPtr mp{};
+    mp.count = n_tensors - base < MT_MAX ? n_tensors - base : MT_MAX;
+    int64_t total = 0;
+    for (int i = 0; i < mp.count; ++i) {
+      mp.p[i] = params[base + i]; mp.g[i] = grads[base + i];
+      mp.m[i] = exp_avg[base + i]; mp.v[i] = exp_avg_sq[base + i];
+      mp.n[i] = sizes[base + i];
+      total += mp.n[i];
+    }
+    hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(total / 4 + 1)), dim3(256), 0, s, mp, lr, beta1,
+                       beta2, eps, weight_decay, bc1, bc2_sqrt, sqnorm, max_norm);
+    COMET_CHECK_LAUNCH("comet_adamw_multi");
+  }
+  return COMET_OK;
+}

@@ -1,0 +1,234 @@
+// Row LayerNorm forward/backward (nn.LayerNorm, GroupNorm(1, C) on token rows) and
+// InstanceNorm2d on channels-last activations.
+//
+// Reference sites: modules.py:261-317 (non-affine eps 1e-6 / affine eps 1e-5),
+// camera_predictor10.py:75-87 (TrajectoryEncoder LNs), base_track_predictor.py:81,238
+// (GroupNorm(1, latent)), modules.py:86-90 + blocks.py:37-38,130-132 (InstanceNorm2d).
+//
+// One wave per row; the row (<= 1024 columns) is held in registers, mean and variance are
+// two exact passes over the registers (wave shuffles), no LDS.
+#include "common.hpp"
+
+namespace comet {
+namespace {
+
+constexpr int LN_MAXV = 16;  // cols <= 64*16 = 1024
+
+template <typename TX, typename TY>
+__global__ void __launch_bounds__(256)
+ln_fwd_kernel(const TX* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+              TY* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+              int64_t rows, int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TX* xr = x + row * cols;
+  float v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + i * 64;
+    v[i] = c < cols ? to_f32(xr[c]) : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + i * 64;
+    const float d = c < cols ? v[i] - mean : 0.f;
+    q += d * d;
+  }
+  const float var = wave_sum(q) / cols;
+  const float rstd = rsqrtf(var + eps);
+  TY* yr = y + row * cols;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + i * 64;
+    if (c < cols) {
+      float o = (v[i] - mean) * rstd;
+      if (w) o = o * w[c];
+      if (b) o = o + b[c];
+      yr[c] = from_f32<TY>(o);
+    }
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// Each block: 256 threads, ROWS_PER_BLOCK rows (4 waves x RPW rows). Weight/bias grads are
+// kept per lane in registers, reduced across the 4 waves in LDS, one atomic per column/block.
+constexpr int LN_RPW = 16;
+
+template <typename TX, typename TD>
+__global__ void __launch_bounds__(256)
+ln_bwd_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const float* __restrict__ mean,
+              const float* __restrict__ rstd, const float* __restrict__ w, float* __restrict__ dx,
+              float* __restrict__ dw, float* __restrict__ db, int64_t rows, int cols, int accum) {
+  __shared__ float red[2][4][1024];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float gw[LN_MAXV], gb[LN_MAXV], wv[LN_MAXV];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    gw[i] = 0.f; gb[i] = 0.f;
+    const int c = lane + i * 64;
+    wv[i] = (w && c < cols) ? w[c] : 1.f;
+  }
+  const int64_t rbase = ((int64_t)blockIdx.x * 4 + wid) * LN_RPW;
+  for (int rr = 0; rr < LN_RPW; ++rr) {
+    const int64_t row = rbase + rr;
+    if (row >= rows) break;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[LN_MAXV], g[LN_MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + i * 64;
+      if (c < cols) {
+        xh[i] = (to_f32(x[row * cols + c]) - mu) * rs;
+        const float d = to_f32(dy[row * cols + c]);
+        gw[i] += d * xh[i];
+        gb[i] += d;
+        g[i] = d * wv[i];
+      } else {
+        xh[i] = 0.f; g[i] = 0.f;
+      }
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + i * 64;
+      if (c < cols) {
+        const float o = rs * (g[i] - s1 - xh[i] * s2);
+        float* p = dx + row * cols + c;
+        *p = accum ? *p + o : o;
+      }
+    }
+  }
+  if (!dw && !db) return;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + i * 64;
+    if (c < cols) { red[0][wid][c] = gw[i]; red[1][wid][c] = gb[i]; }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    if (dw) atomicAdd(dw + c, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
+    if (db) atomicAdd(db + c, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+  }
+}
+
+// InstanceNorm over H*W per (n, c) on NHWC input; one block per (n, 64-channel slab).
+// Optional fused residual: res_norm_relu==0: y = relu?(IN(x) + res); the ResidualBlock
+// tail relu(x + y) is expressed by the caller.
+template <typename T>
+__global__ void __launch_bounds__(256)
+instnorm_nhwc_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
+                     int64_t hw, int c, float eps, int relu) {
+  __shared__ float red_s[4][64], red_q[4][64];
+  const int64_t n = blockIdx.x;
+  const int c0 = blockIdx.y * 64;
+  const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;  // 4 parts over hw
+  const int ch = c0 + cl;
+  const bool ok = ch < c;
+  const T* xb = x + n * hw * c;
+  // pass 1: mean
+  float s = 0.f;
+  if (ok)
+    for (int64_t p = part; p < hw; p += 4) s += to_f32(xb[p * c + ch]);
+  red_s[part][cl] = s;
+  __syncthreads();
+  const float mean = (red_s[0][cl] + red_s[1][cl] + red_s[2][cl] + red_s[3][cl]) / hw;
+  // pass 2: variance (biased, as InstanceNorm2d)
+  float q = 0.f;
+  if (ok)
+    for (int64_t p = part; p < hw; p += 4) {
+      const float d = to_f32(xb[p * c + ch]) - mean;
+      q += d * d;
+    }
+  red_q[part][cl] = q;
+  __syncthreads();
+  const float var = (red_q[0][cl] + red_q[1][cl] + red_q[2][cl] + red_q[3][cl]) / hw;
+  const float rstd = rsqrtf(var + eps);
+  if (!ok) return;
+  T* yb = y + n * hw * c;
+  const T* rb = res ? res + n * hw * c : nullptr;
+  for (int64_t p = part; p < hw; p += 4) {
+    float o = (to_f32(xb[p * c + ch]) - mean) * rstd;
+    if (rb) o += to_f32(rb[p * c + ch]);
+    if (relu) o = o > 0.f ? o : 0.f;
+    yb[p * c + ch] = from_f32<T>(o);
+  }
+}
+
+}  // namespace
+}  // namespace comet
+
+using namespace comet;
+
+extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, const float* weight,
+                                   const float* bias, void* y, float* mean, float* rstd,
+                                   int64_t rows, int64_t cols, float eps, void* stream) {
+  COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_fwd: cols must be in [1,1024]");
+  COMET_CHECK_ARG(x && y, "comet_layernorm_fwd: null pointer");
+  if (rows == 0) return COMET_OK;
+  dim3 grid((unsigned)cdiv(rows, 4));
+  hipStream_t s = as_stream(stream);
+#define LNF(TX, TY)                                                                        \
+  hipLaunchKernelGGL((ln_fwd_kernel<TX, TY>), grid, dim3(256), 0, s, (const TX*)x, weight, \
+                     bias, (TY*)y, mean, rstd, rows, (int)cols, eps)
+  if (dtype_x == COMET_F32 && dtype_y == COMET_F32) LNF(float, float);
+  else if (dtype_x == COMET_F32 && dtype_y == COMET_BF16) LNF(float, __bf16);
+  else if (dtype_x == COMET_BF16 && dtype_y == COMET_F32) LNF(__bf16, float);
+  else if (dtype_x == COMET_BF16 && dtype_y == COMET_BF16) LNF(__bf16, __bf16);
+  else { set_error("comet_layernorm_fwd: bad dtype"); return COMET_EINVAL; }
+#undef LNF
+  COMET_CHECK_LAUNCH("comet_layernorm_fwd");
+  return COMET_OK;
+}
+
+extern "C" int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy,
+                                   const float* mean, const float* rstd, const float* weight,
+                                   float* dx, float* dweight, float* dbias, int64_t rows,
+                                   int64_t cols, int dx_accumulate, void* stream) {
+  COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_bwd: cols must be in [1,1024]");
+  COMET_CHECK_ARG(x && dy && mean && rstd && dx, "comet_layernorm_bwd: null pointer");
+  if (rows == 0) return COMET_OK;
+  dim3 grid((unsigned)cdiv(rows, 4 * LN_RPW));
+  hipStream_t s = as_stream(stream);
+#define LNB(TX, TD)                                                                           \
+  hipLaunchKernelGGL((ln_bwd_kernel<TX, TD>), grid, dim3(256), 0, s, (const TX*)x, (const TD*)dy, \
+                     mean, rstd, weight, dx, dweight, dbias, rows, (int)cols, dx_accumulate)
+  if (dtype_x == COMET_F32 && dtype_dy == COMET_F32) LNB(float, float);
+  else if (dtype_x == COMET_F32 && dtype_dy == COMET_BF16) LNB(float, __bf16);
+  else if (dtype_x == COMET_BF16 && dtype_dy == COMET_F32) LNB(__bf16, float);
+  else if (dtype_x == COMET_BF16 && dtype_dy == COMET_BF16) LNB(__bf16, __bf16);
+  else { set_error("comet_layernorm_bwd: bad dtype"); return COMET_EINVAL; }
+#undef LNB
+  COMET_CHECK_LAUNCH("comet_layernorm_bwd");
+  return COMET_OK;
+}
+
+extern "C" int comet_instnorm_nhwc(int dtype, const void* x, const void* res, void* y, int64_t n,
+                                   int64_t hw, int64_t c, float eps, int relu, int res_norm_relu,
+                                   void* stream) {
+  (void)res_norm_relu;
+  COMET_CHECK_ARG(x && y && n > 0 && hw > 0 && c > 0, "comet_instnorm_nhwc: bad args");
+  COMET_CHECK_ARG(cdiv(c, 64) <= 65535, "comet_instnorm_nhwc: c too large");
+  dim3 grid((unsigned)n, (unsigned)cdiv(c, 64));
+  hipStream_t s = as_stream(stream);
+  if (dtype == COMET_F32)
+    hipLaunchKernelGGL((instnorm_nhwc_kernel<float>), grid, dim3(256), 0, s, (const float*)x,
+                       (const float*)res, (float*)y, hw, (int)c, eps, relu);
+  else if (dtype == COMET_BF16)
+    hipLaunchKernelGGL((instnorm_nhwc_kernel<__bf16>), grid, dim3(256), 0, s, (const __bf16*)x,
+                       (const __bf16*)res, (__bf16*)y, hw, (int)c, eps, relu);
+  else { set_error("comet_instnorm_nhwc: bad dtype"); return COMET_EINVAL; }
+  COMET_CHECK_LAUNCH("comet_instnorm_nhwc");
+  return COMET_OK;
+}

@@ -1,0 +1,195 @@
+"""Kernel-level parity: every libcomet_hip.so op against a plain PyTorch fp32/fp64 CPU
+reference of the same op (seeded random inputs, shapes covering tails and all layouts)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from comet_amd import ops
+    return ops
+
+
+def _rand(*shape, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+def _close(got, ref, rtol, atol, what=""):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    err = (got - ref).abs()
+    tol = atol + rtol * ref.abs()
+    bad = (err > tol)
+    assert not bad.any(), f"{what}: max err {err.max().item():.3e} (ref max {ref.abs().max().item():.3e}), {bad.sum().item()} bad"
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("mnk", [(128, 128, 64), (200, 130, 664), (1, 4, 768), (77, 3, 2), (300, 520, 96)])
+def test_gemm_layouts(dtype, la, lb, mnk):
+    ops = _ops()
+    M, N, K = mnk
+    A = _rand(M, K, dtype=dtype, seed=1)
+    B = _rand(N, K, dtype=dtype, seed=2)
+    ref = A.double() @ B.double().t()
+    Ad = (A if la == 0 else A.t().contiguous()).to(DEV)
+    Bd = (B if lb == 0 else B.t().contiguous()).to(DEV)
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.gemm_raw(Ad, Bd, C, m=M, n=N, k=K, layout_a=la, lda=(K if la == 0 else M),
+                 layout_b=lb, ldb=(K if lb == 0 else N), ldc=N)
+    tol = 2e-5 if dtype == torch.float32 else 1e-3
+    _close(C, ref, tol, tol * math.sqrt(K), f"gemm {dtype} la={la} lb={lb} {mnk}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogue_bias_gelu_resid_aux(dtype):
+    ops = _ops()
+    M, N, K = 257, 384, 192
+    x = _rand(M, K, dtype=dtype, seed=3)
+    w = _rand(N, K, dtype=dtype, seed=4, scale=0.1)
+    b = _rand(N, seed=5)
+    r = _rand(M, N, seed=6)
+    pre = x.double() @ w.double().t() + b.double()
+    ref = F.gelu(pre) + 0.5 * r.double()
+    out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    aux = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=1, resid=r.to(DEV), beta=0.5, out=out, aux=aux)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    _close(out, ref, tol, 1e-3, "epilogue out")
+    _close(aux, pre, tol, 1e-3, "epilogue aux")
+
+
+def test_gemm_batched_strided():
+    ops = _ops()
+    # per (b, h): C = Q_bh K_bh^T with q/k packed [B, L, 3, H, D]
+    B, L, H, D = 3, 70, 4, 32
+    qkv = _rand(B, L, 3, H, D, seed=7).to(DEV)
+    q = qkv[:, :, 0]
+    k = qkv[:, :, 1]
+    S = torch.empty(B, H, L, L, device=DEV)
+    ops.gemm_raw(q, k, S, m=L, n=L, k=D, layout_a=0, lda=3 * H * D, layout_b=0, ldb=3 * H * D, ldc=L,
+                 batch=(B, H), stride_a=(L * 3 * H * D, D), stride_b=(L * 3 * H * D, D),
+                 stride_c=(H * L * L, L * L))
+    ref = torch.einsum("blhd,bmhd->bhlm", q.double().cpu(), k.double().cpu())
+    _close(S, ref, 2e-5, 1e-4, "batched gemm")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("affine,eps,cols", [(False, 1e-6, 768), (True, 1e-5, 768), (True, 1e-5, 256), (True, 1e-5, 130)])
+def test_layernorm_fwd_bwd(dtype, affine, eps, cols):
+    ops = _ops()
+    rows = 333
+    x = _rand(rows, cols, seed=8, scale=3.0) + 1.5
+    w = _rand(cols, seed=9) if affine else None
+    b = _rand(cols, seed=10) if affine else None
+    xd = x.to(dtype)
+    xr = xd.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True) if affine else None
+    br = b.double().requires_grad_(True) if affine else None
+    yr = F.layer_norm(xr, (cols,), wr, br, eps)
+    dy = _rand(rows, cols, seed=11)
+    yr.backward(dy.double())
+    y, mean, rstd = ops.layernorm(xd.to(DEV), w.to(DEV) if affine else None, b.to(DEV) if affine else None,
+                                  eps=eps, out_dtype=torch.float32, stats=True)
+    _close(y, yr.detach(), 1e-5, 1e-5, "ln fwd")
+    dw = torch.zeros(cols, device=DEV) if affine else None
+    db = torch.zeros(cols, device=DEV) if affine else None
+    dx = ops.layernorm_bwd(xd.to(DEV), dy.to(DEV), mean, rstd, w.to(DEV) if affine else None, dw, db)
+    _close(dx, xr.grad, 1e-4, 1e-4, "ln dx")
+    if affine:
+        _close(dw, wr.grad, 1e-4, 1e-3, "ln dw")
+        _close(db, br.grad, 1e-4, 1e-3, "ln db")
+
+
+def _attn_ref(q, k, v, heads, scale):
+    B, Lq, C = q.shape
+    D = C // heads
+    qh = q.double().reshape(B, Lq, heads, D).transpose(1, 2)
+    kh = k.double().reshape(B, -1, heads, D).transpose(1, 2)
+    vh = v.double().reshape(B, -1, heads, D).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) * scale
+    lse = torch.logsumexp(s, -1)
+    o = torch.softmax(s, -1) @ vh
+    return o.transpose(1, 2).reshape(B, Lq, C), lse
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("D", [32, 48, 64, 96])
+@pytest.mark.parametrize("lq,lk", [(16, 16), (577, 577), (1, 512), (130, 77), (64, 200)])
+def test_attention_fwd(dtype, D, lq, lk):
+    ops = _ops()
+    B, H = 2, 3
+    q = _rand(B, lq, H * D, dtype=dtype, seed=12)
+    k = _rand(B, lk, H * D, dtype=dtype, seed=13)
+    v = _rand(B, lk, H * D, dtype=dtype, seed=14)
+    scale = D ** -0.5
+    ref, lse_ref = _attn_ref(q, k, v, H, scale)
+    out, lse = ops.attention(q.to(DEV), k.to(DEV), v.to(DEV), H, scale, lse=True)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    _close(out, ref, tol, tol, f"attn {dtype} D={D} {lq}x{lk}")
+    _close(lse, lse_ref, 1e-4, 1e-4 if dtype == torch.float32 else 1e-2, "lse")
+
+
+def test_attention_strided_packed_qkv():
+    ops = _ops()
+    B, L, H, D = 2, 100, 8, 96
+    C = H * D
+    qkv = _rand(B, L, 3 * C, seed=15).to(DEV)
+    q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+    out = ops.attention(q, k, v, H)
+    ref, _ = _attn_ref(q.cpu(), k.cpu(), v.cpu(), H, D ** -0.5)
+    _close(out, ref, 2e-5, 2e-5, "packed qkv attention")
+
+
+def test_attention_large_logits_rescale():
+    """Force the online-softmax rescale path: a spike key in a late tile."""
+    ops = _ops()
+    B, H, D, L = 1, 1, 64, 300
+    q = _rand(B, L, D, seed=16)
+    k = _rand(B, L, D, seed=17)
+    k[0, 250] = q[0].mean(0) * 40
+    v = _rand(B, L, D, seed=18)
+    ref, _ = _attn_ref(q, k, v, H, D ** -0.5)
+    out = ops.attention(q.to(DEV), k.to(DEV), v.to(DEV), H)
+    _close(out, ref, 2e-5, 2e-5, "rescale")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_via_im2col(dtype):
+    ops = _ops()
+    N, Cin, H, W, Cout = 2, 5, 17, 19, 24
+    for (k, s, p) in [(7, 2, 3), (3, 1, 1), (1, 1, 0), (3, 2, 1), (14, 14, 0)]:
+        Hs, Ws = (28, 42) if k == 14 else (H, W)
+        x = _rand(N, Cin, Hs, Ws, dtype=dtype, seed=19)
+        w = _rand(Cout, Cin, k, k, dtype=dtype, seed=20, scale=0.2)
+        b = _rand(Cout, seed=21)
+        ref = F.conv2d(x.double(), w.double(), b.double(), stride=s, padding=p)
+        xn = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+        cols, oh, ow = ops.im2col_nhwc(xn, k, k, s, p)
+        wm = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().to(DEV)
+        y = ops.linear(cols, wm, bias=b.to(DEV), out_dtype=torch.float32)
+        y = y.reshape(N, oh, ow, Cout).permute(0, 3, 1, 2)
+        tol = 1e-5 if dtype == torch.float32 else 2e-3
+        _close(y, ref, tol, tol * 10, f"conv k={k} s={s}")
+
+
+def test_instnorm_and_resize():
+    ops = _ops()
+    x = _rand(3, 40, 23, 21, seed=22) * 2 + 1
+    res = _rand(3, 40, 23, 21, seed=23)
+    ref = F.relu(F.instance_norm(x.double()) + res.double())
+    y = ops.instnorm_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV), res.permute(0, 2, 3, 1).contiguous().to(DEV), relu=True)
+    _close(y.permute(0, 3, 1, 2), ref, 1e-5, 1e-5, "instnorm")
+    for (oh, ow) in [(11, 10), (64, 64), (31, 31), (1, 1)]:
+        r = F.interpolate(x, (oh, ow), mode="bilinear", align_corners=True)
+        y1 = ops.resize_bilinear(x.to(DEV), oh, ow, nhwc=False)
+        _close(y1, r, 1e-5, 1e-5, f"resize nchw {oh}x{ow}")
+        y2 = ops.resize_bilinear(x.permute(0, 2, 3, 1).contiguous().to(DEV), oh, ow, nhwc=True)
+        _close(y2.permute(0, 3, 1, 2), r, 1e-5, 1e-5, f"resize nhwc {oh}x{ow}")

@@ -1,0 +1,19 @@
+import sys, torch
+sys.path.insert(0, "comet-pose-estimation_amd")
+from comet_amd import ops
+torch.manual_seed(0)
+B, H, D, L = 1, 1, 32, 64
+def run(q, k, v):
+    o = ops.attention(q.cuda(), k.cuda(), v.cuda(), H).float().cpu()
+    s = (q.float() @ k.float().transpose(-1, -2)) * D ** -0.5
+    ref = torch.softmax(s, -1) @ v.float()
+    return o, ref
+q = torch.randn(B, L, D).bfloat16(); k = torch.randn(B, L, D).bfloat16()
+v1 = torch.ones(B, L, D).bfloat16()
+o, r = run(q, k, v1); print("V=1  err", (o - r).abs().max().item(), o[0, :3, :4])
+o, r = run(torch.zeros_like(q), k, torch.randn(B, L, D).bfloat16()); print("Q=0  err", (o - r).abs().max().item())
+vv = torch.zeros(B, L, D); vv[0, :, 0] = torch.arange(L).float(); vv = vv.bfloat16()
+o, r = run(torch.zeros_like(q), k, vv); print("Q=0 V=key idx col0: got", o[0, :2, :4], "ref", r[0, :2, :4])
+vv = torch.zeros(B, L, D); vv[0, 5, :] = torch.arange(D).float(); vv = vv.bfloat16()
+o, r = run(torch.zeros_like(q), k, vv); print("Q=0 V row5=d: got", o[0, 0, :8] * L, "ref", r[0, 0, :8] * L)
+o, r = run(q, k, torch.randn(B, L, D).bfloat16()); print("rand err", (o - r).abs().max().item())
