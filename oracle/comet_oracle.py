@@ -644,10 +644,9 @@ def train_step(P_train, P_all, image, tracks, gt, lr=1e-5, state=None, max_norm=
     grads = [torch.zeros_like(params[k]) if g is None else g for k, g in zip(names, grads)]
     total = torch.norm(torch.stack([torch.norm(g, 2.0) for g in grads]), 2.0)
     coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
-    grads = [g * coef for g in grads]
     opt_params = [params[k].detach().clone() for k in names]
     opt = torch.optim.AdamW(opt_params, lr=lr)
     for p, g in zip(opt_params, grads):
-        p.grad = g
+        p.grad = g * coef
     opt.step()
     return loss.detach(), dict(zip(names, grads)), dict(zip(names, opt_params)), total

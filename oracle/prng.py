@@ -76,9 +76,40 @@ def param_value(seed: int, name: str, shape) -> torch.Tensor:
         v = 1.0 + 0.1 * u
     else:
         v = 0.05 * u
+    if ".updateformer.flow_head." in name:
+        # parity-friendly damping: random-weight tracker iterations are chaotic (an fp32 ulp at
+        # iteration 0 grows ~100x per iteration); small coordinate/feature updates keep the
+        # reference, the oracle and the HIP path comparable after 4-6 iterations.
+        v = v * FLOW_HEAD_DAMP
     return torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32))
+
+
+FLOW_HEAD_DAMP = 0.01
 
 
 def make_state_dict(seed: int, shapes: dict) -> dict:
     """shapes: name -> shape (e.g. {k: v.shape for k, v in model.state_dict().items()})."""
     return {k: param_value(seed, k, s) for k, s in shapes.items()}
+
+
+def synthetic_batch(seed: int, B: int, T: int, H: int, W: int, N: int):
+    """Synthetic inputs of SURVEY.md §8(d): images ~N(0,1) (post-normalisation distribution),
+    kp0 ~ U[0, W-1]^2 broadcast over T, unit quaternions (w >= 0), T_uvz = (U[270,370],
+    U[190,290], U[5,15]), T_xyz ~ N(0,1), focal 268.44, ratio 0.5 (float64, as collated)."""
+    img = torch.from_numpy(normal_like(seed, "images", (B, T, 3, H, W)))
+    kp = (uniform(seed, "kp0", (B, N, 2)) + 1.0) * 0.5 * np.float32(W - 1)
+    tracks = torch.from_numpy(kp).unsqueeze(1).expand(B, T, N, 2).contiguous()
+    q = normal_like(seed, "quat", (B * T, 4)).astype(np.float64)
+    q /= np.linalg.norm(q, axis=-1, keepdims=True)
+    q[q[:, 0] < 0] *= -1
+    u = uniform(seed, "uvz", (B * T, 3))
+    uvz = np.stack([320 + 50 * u[:, 0], 240 + 50 * u[:, 1], 10 + 5 * u[:, 2]], -1).astype(np.float32)
+    gt = {
+        "R": torch.from_numpy(q.astype(np.float32)),
+        "T_uvz": torch.from_numpy(uvz),
+        "T": torch.from_numpy(normal_like(seed, "txyz", (B * T, 3))),
+        "focal_length": torch.full((B * T, 2), 268.44),
+        "principal_point": torch.zeros(B * T, 2),
+        "ratio": torch.tensor([0.5], dtype=torch.float64),
+    }
+    return img, tracks, gt

@@ -1,0 +1,226 @@
+"""Generate tests/golden/*.npz from the REFERENCE itself (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tools/gen_golden.py
+
+Refuses to run without /root/reference. Weights come from oracle/prng.py (seeded; fixtures
+store only seeds and outputs), inputs from oracle.prng.synthetic_batch. Also cross-checks the
+oracle restatement against the reference on the same inputs and prints the max differences.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+import ref_harness as H  # noqa: E402
+from oracle import prng  # noqa: E402
+from oracle import comet_oracle as O  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+SEED_W, SEED_X = 0, 1
+CFG_SMALL = dict(B=1, T=4, H=128, W=128, N=16)
+
+
+def reference_shapes(model):
+    """state_dict layout of the reference COMET in checkpoint (facebookresearch DINOv2) naming."""
+    shapes = {}
+    for k, v in model.state_dict().items():
+        if k.startswith("camera_predictor.backbone."):
+            if k == "camera_predictor.backbone.model.embeddings.cls_token":
+                shapes.update(H.dinov2_fb_shapes())
+            continue
+        shapes[k] = tuple(v.shape)
+    return shapes
+
+
+def reference_state(model, seed):
+    """PRNG state dict in facebookresearch naming (= product naming) + its stand-in conversion."""
+    P = prng.make_state_dict(seed, reference_shapes(model))
+    return P, H.fb_to_hf(P)
+
+
+def np32(t):
+    return t.detach().float().cpu().numpy().astype(np.float32)
+
+
+def put_grad(out, prefix, k, g):
+    """small grads in full; large ones as L2 norm + the first 4 rows."""
+    out[prefix + "norm." + k] = np.array([g.double().norm().item()])
+    out[prefix + ("" if g.numel() <= 4096 else "head.") + k] = np32(g if g.numel() <= 4096 else g.reshape(g.shape[0], -1)[:4])
+
+
+def gen_end_to_end(out):
+    torch.manual_seed(0)
+    cfg = H.load_cfg()
+    model = H.build_reference_comet(cfg)
+    P, P_hf = reference_state(model, SEED_W)
+    missing, unexpected = model.load_state_dict(P_hf, strict=True), None
+    q = CFG_SMALL
+    img, tracks, gt = prng.synthetic_batch(SEED_X, q["B"], q["T"], q["H"], q["W"], q["N"])
+    QC = H.reference_module("train_eval_func_new_cp5").QuaternionCameras
+    cams = QC(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+              principal_point=gt["principal_point"], ratio=gt["ratio"])
+    cap = {}
+
+    def hook(name):
+        def f(m, i, o):
+            cap[name] = o["x_norm_patchtokens"] if isinstance(o, dict) else o
+        return f
+    model.track_predictor.coarse_fnet.register_forward_hook(hook("fmaps"))
+    model.track_predictor.fine_fnet.register_forward_hook(hook("patch_feat"))
+    model.camera_predictor.backbone.register_forward_hook(hook("tokens"))
+    model.camera_predictor.trunk.register_forward_hook(hook("trunk_out"))
+    model.camera_predictor.cross_attn_block[0].register_forward_hook(hook("tp0_out"))
+
+    pred = model(img, gt_cameras=cams, training=True, tracks=tracks,
+                 tracks_visibility=torch.ones(q["B"], q["T"], q["N"], dtype=torch.bool))
+    loss = pred["loss"].mean()
+    model.zero_grad()
+    loss.backward()
+    grads = {k: p.grad for k, p in model.camera_predictor.named_parameters() if p.grad is not None}
+
+    out["e2e_pred_pose_enc"] = np32(pred["pred_pose_enc"])
+    out["e2e_gt_pose_enc"] = np32(pred["gt_pose_enc"])
+    out["e2e_loss"] = np32(pred["loss"].reshape(1))
+    out["e2e_loss_trans"] = np32(pred["loss_trans"].reshape(1))
+    out["e2e_loss_rot"] = np32(pred["loss_rot"].reshape(1))
+    out["e2e_pred_R"] = np32(pred["pred_cameras"].R)
+    out["e2e_pred_T"] = np32(pred["pred_cameras"].T)
+    out["e2e_pred_tracks"] = np32(pred["pred_tracks"])
+    out["e2e_fmaps"] = np32(cap["fmaps"])
+    pf = cap["patch_feat"]
+    out["e2e_patch_feat_head"] = np32(pf[:8])
+    out["e2e_patch_feat_sum"] = np32(pf.double().sum().reshape(1))
+    out["e2e_patch_feat_abssum"] = np32(pf.double().abs().sum().reshape(1))
+    tok = cap["tokens"]
+    out["e2e_tokens_head"] = np32(tok[:, :8])
+    out["e2e_tokens_sum"] = np32(tok.double().sum(dim=(1, 2)))
+    out["e2e_trunk_out"] = np32(cap["trunk_out"])
+    out["e2e_tp0_out"] = np32(cap["tp0_out"])
+    names = sorted(grads)
+    out["grad_names"] = np.array(names)
+    out["grad_norms"] = np.array([grads[k].double().norm().item() for k in names])
+    for k in ["fc_depth.weight", "fc_translation2d.weight", "pose_branch.fc2.weight", "pose_token",
+              "trunk.3.mlp.fc2.bias", "confidence_attention.0.weight", "traj_encoder.mlp.0.weight"]:
+        out["grad_full." + k] = np32(grads[k])
+
+    # --- cross-check the oracle restatement on the same inputs ---
+    gt_o = dict(gt)
+    res = O.comet_forward(P, img, tracks, gt_o, return_all=True)
+    diffs = {
+        "pred_pose_enc": (res["pred_pose_enc"] - pred["pred_pose_enc"]).abs().max().item(),
+        "loss": abs(res["loss"].item() - loss.item()),
+        "pred_tracks": (res["pred_tracks"] - pred["pred_tracks"]).abs().max().item(),
+        "pred_T": (res["pred_T"] - pred["pred_cameras"].T).abs().max().item(),
+        "fmaps": (res["fmaps"].reshape(cap["fmaps"].shape) - cap["fmaps"]).abs().max().item(),
+    }
+    print("oracle vs reference (fp32):", {k: f"{v:.2e}" for k, v in diffs.items()})
+    train_names = ["camera_predictor." + k for k in names]
+    _, g_o, _, _ = O.train_step(train_names, P, img, tracks, gt_o)
+    gd = max((g_o["camera_predictor." + k] - grads[k]).abs().max().item() / (grads[k].abs().max().item() + 1e-12) for k in names)
+    print(f"oracle vs reference grads: max rel-to-max diff {gd:.2e}")
+
+    # --- bf16 autocast run of the reference (accelerate mixed_precision='bf16') ---
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        pb = model(img, gt_cameras=cams, training=True, tracks=tracks,
+                   tracks_visibility=torch.ones(q["B"], q["T"], q["N"], dtype=torch.bool))
+    out["bf16_pred_pose_enc"] = np32(pb["pred_pose_enc"].float())
+    out["bf16_loss"] = np32(pb["loss"].float().reshape(1))
+    out["bf16_pred_tracks"] = np32(pb["pred_tracks"].float())
+    out["cfg"] = np.array([SEED_W, SEED_X, q["B"], q["T"], q["H"], q["W"], q["N"]])
+    return model, P
+
+
+def gen_blocks(out):
+    """G1: AttnBlock / CrossAttnBlock of modules.py with PRNG weights: outputs + all grads."""
+    mod = H.reference_module("models.modules")
+    torch.manual_seed(0)
+    blk = mod.AttnBlock(768, 8, mlp_ratio=4)
+    P = prng.make_state_dict(SEED_W + 7, {k: tuple(v.shape) for k, v in blk.state_dict().items()})
+    blk.load_state_dict(P)
+    x = torch.from_numpy(prng.normal_like(SEED_X + 7, "attn_x", (3, 37, 768))).requires_grad_(True)
+    y = blk(x)
+    gy = torch.from_numpy(prng.normal_like(SEED_X + 7, "attn_gy", (3, 37, 768)))
+    y.backward(gy)
+    out["blk_attn_y"] = np32(y)
+    out["blk_attn_dx"] = np32(x.grad)
+    for k, p in blk.named_parameters():
+        put_grad(out, "blk_attn_grad.", k, p.grad)
+    cblk = mod.CrossAttnBlock(768, 768, 8, mlp_ratio=4)
+    P = prng.make_state_dict(SEED_W + 8, {k: tuple(v.shape) for k, v in cblk.state_dict().items()})
+    cblk.load_state_dict(P)
+    x = torch.from_numpy(prng.normal_like(SEED_X + 8, "cx", (2, 29, 768))).requires_grad_(True)
+    c = torch.from_numpy(prng.normal_like(SEED_X + 8, "cc", (2, 41, 768))).requires_grad_(True)
+    y = cblk(x, c)
+    gy = torch.from_numpy(prng.normal_like(SEED_X + 8, "cgy", (2, 29, 768)))
+    y.backward(gy)
+    out["blk_cross_y"] = np32(y)
+    out["blk_cross_dx"] = np32(x.grad)
+    out["blk_cross_dctx"] = np32(c.grad)
+    for k, p in cblk.named_parameters():
+        put_grad(out, "blk_cross_grad.", k, p.grad)
+
+
+def gen_exact(out):
+    """G5: sincos tables, HarmonicEmbedding, pose codec vectors straight from the reference."""
+    ut = H.reference_module("utils")
+    he = H.reference_module("minipytorch3d.harmonic_embedding")
+    out["sincos_1d_768_16"] = np32(ut.get_1d_sincos_pos_embed(768, 16))
+    out["sincos_2d_768_24"] = np32(ut.get_2d_sincos_pos_embed(768, (24, 24)))
+    out["sincos_2d_664_16"] = np32(ut.get_2d_sincos_pos_embed(664, (16, 16)))
+    xy = torch.from_numpy(prng.uniform(SEED_X, "flows", (5, 7, 2)) * 20)
+    out["embed2d_in"] = np32(xy)
+    out["embed2d_64"] = np32(ut.get_2d_embedding(xy, 64, cat_coords=False))
+    x = torch.from_numpy(prng.uniform(SEED_X, "harm_x", (4, 5, 8)) * 3)
+    cov = torch.from_numpy(np.abs(prng.uniform(SEED_X, "harm_cov", (4, 5, 8))) * 0.1)
+    out["harm_x"] = np32(x)
+    out["harm_cov"] = np32(cov)
+    for n, om, logs, app in [(6, 1.0, True, True), (48, 1.0, True, False), (10, 0.5, False, True)]:
+        m = he.HarmonicEmbedding(n_harmonic_functions=n, omega_0=om, logspace=logs, append_input=app)
+        tag = f"harm_{n}_{om}_{int(logs)}_{int(app)}"
+        out[tag] = np32(m(x))
+        out[tag + "_cov"] = np32(m(x, diag_cov=cov))
+    # pose codec (utils.py:312-403, 631-688) for one 6-frame sequence
+    _, _, gt = prng.synthetic_batch(SEED_X + 3, 1, 6, 64, 64, 4)
+    QC = H.reference_module("train_eval_func_new_cp5").QuaternionCameras
+    cams = QC(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+              principal_point=gt["principal_point"], ratio=gt["ratio"])
+    enc = ut.camera_to_pose_encoding2(cams)
+    out["codec_gt_R"] = np32(gt["R"])
+    out["codec_gt_Tuvz"] = np32(gt["T_uvz"])
+    out["codec_enc"] = np32(enc)
+    penc = torch.from_numpy(prng.uniform(SEED_X + 3, "penc", (1, 6, 7)) * 0.3)
+    penc[..., 3:7] = torch.nn.functional.normalize(penc[..., 3:7] + torch.tensor([1.0, 0, 0, 0]), dim=-1)
+    out["codec_penc"] = np32(penc)
+    for it in ["AMD_eval", "AMD_test", "spark"]:
+        pc = ut.pose_encoding_to_camera2(penc, gt_cameras=cams, pose_encoding_type="absT_quaR_OneFL",
+                                         to_OpenCV=False, intri_type=it)
+        out[f"codec_dec_R_{it}"] = np32(pc.R)
+        out[f"codec_dec_T_{it}"] = np32(pc.T)
+
+
+def main():
+    H.require_reference()
+    os.makedirs(OUT, exist_ok=True)
+    torch.set_num_threads(8)
+    out = {}
+    gen_exact(out)
+    gen_blocks(out)
+    gen_end_to_end(out)
+    import json
+    cfg = H.load_cfg()
+    shapes = reference_shapes(H.build_reference_comet(cfg))
+    with open(os.path.join(OUT, "comet_state_dict_shapes.json"), "w") as f:
+        json.dump([[k, list(v)] for k, v in shapes.items()], f, indent=0)
+    path = os.path.join(OUT, "comet_golden_v1.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
+if __name__ == "__main__":
+    main()
