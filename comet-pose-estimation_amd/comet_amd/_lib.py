@@ -50,7 +50,7 @@ SIGNATURES = {
     "comet_version": (_INT, []),
     "comet_last_error": (ctypes.c_char_p, []),
     "comet_gemm": (_INT, [ctypes.POINTER(GemmArgs), c_vp]),
-    "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, _F, c_vp]),
+    "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _F, _INT, c_vp]),
     "comet_layernorm_bwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, _INT, c_vp]),
     "comet_attention_fwd": (_INT, [ctypes.POINTER(AttnArgs), c_vp]),
     "comet_attn_probs": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _F, c_vp]),
@@ -65,6 +65,31 @@ SIGNATURES = {
     "comet_im2col_nhwc": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _INT, _INT, _INT, _INT, c_i64, c_i64, c_i64, c_vp]),
     "comet_instnorm_nhwc": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, _F, _INT, _INT, c_vp]),
     "comet_resize_bilinear": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, _INT, c_vp]),
+    "comet_act_fwd": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_vp]),
+    "comet_binary": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_i64, c_vp]),
+    "comet_add_rows": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "comet_rowscale_fwd": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "comet_rowscale_bwd": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
+    "comet_sincos_table": (_INT, [c_vp, c_vp, c_i64, _INT, c_i64, c_i64, c_vp]),
+    "comet_harmonic_fwd": (_INT, [c_vp, c_vp, c_vp, c_vp, c_i64, _INT, _INT, _INT, c_vp]),
+    "comet_harmonic_bwd": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, _INT, _INT, c_vp]),
+    "comet_pose_encode": (_INT, [c_vp, c_vp, c_vp, ctypes.c_double, c_vp, c_i64, _INT, c_vp]),
+    "comet_pose_decode": (_INT, [c_vp, c_vp, c_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_i64, _INT, c_vp]),
+    "comet_gapr_fwd": (_INT, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, _INT, _INT, _F, _F, c_vp]),
+    "comet_gapr_bwd": (_INT, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, _INT, _INT,
+                              _F, _F, c_vp]),
+    "comet_sample_bilinear": (_INT, [_INT, c_vp, c_i64, _INT, _INT, _INT, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64,
+                                     c_i64, c_i64, _INT, c_vp]),
+    "comet_corr_sample": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, _INT, _INT, _INT, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                 c_i64, c_i64, _INT, c_vp]),
+    "comet_tracker_tokens": (_INT, [_INT, c_vp, c_vp, _INT, c_vp, c_i64, _INT, c_vp, _INT, c_vp, c_i64, _INT, c_vp]),
+    "comet_coords_update": (_INT, [_INT, c_vp, c_vp, c_i64, c_vp, _F, c_i64, c_i64, _INT, c_vp]),
+    "comet_avgpool2_nhwc": (_INT, [_INT, c_vp, c_vp, c_i64, _INT, _INT, _INT, c_vp]),
+    "comet_patch_gather": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_i64, _INT, _INT, _INT, c_vp]),
+    "comet_refine_combine": (_INT, [c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_i64, c_vp]),
+    "comet_track_score": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_i64, _INT, _INT, _INT, c_vp]),
+    "comet_dino_prep": (_INT, [_INT, c_vp, c_vp, c_i64, _INT, _INT, _INT, _INT, c_i64, c_vp, c_vp, c_vp]),
 }
 
 _lib = None

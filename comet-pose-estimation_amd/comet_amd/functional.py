@@ -1,0 +1,447 @@
+"""Differentiable operators of the hot path, forward AND backward on libcomet_hip.so.
+
+Each op is a torch.autograd.Function whose forward/backward only call comet kernels (torch is
+used for allocation and views). Under no_grad (tracker, DINOv2) the same functions run the
+forward kernels without building a graph.
+
+Precision policy (mirrors accelerate mixed_precision="bf16" autocast, abl_ours.yaml:102):
+  * compute dtype COMPUTE (bf16 by default, f32 for parity runs): GEMM / attention operands;
+  * residual stream, LayerNorm statistics and outputs, softmax statistics, losses and all
+    gradients w.r.t. parameters: f32.
+"""
+import contextlib
+import threading
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+_state = threading.local()
+
+
+def compute_dtype():
+    return getattr(_state, "dtype", torch.bfloat16)
+
+
+@contextlib.contextmanager
+def precision(dtype):
+    old = compute_dtype()
+    _state.dtype = dtype
+    try:
+        yield
+    finally:
+        _state.dtype = old
+
+
+# ------------------------------------------------------------------------------------------
+# weight copies in the compute dtype (cast once, invalidated after every optimizer step)
+# ------------------------------------------------------------------------------------------
+_wcache = {}
+
+
+def wcast(p):
+    """p (an f32 parameter or a view of one) in the compute dtype; cached by storage address
+    and shape, so the frozen tracker / DINOv2 weights are cast once."""
+    dt = compute_dtype()
+    if p.dtype == dt:
+        return p
+    key = (p.data_ptr(), tuple(p.shape), tuple(p.stride()), dt)
+    hit = _wcache.get(key)
+    if hit is not None:
+        return hit
+    c = ops.cast(p.detach(), dt)
+    _wcache[key] = c
+    return c
+
+
+def invalidate_weight_cache(params=None):
+    """Drop cached copies of `params` (all when None); called after every optimizer step."""
+    if params is None:
+        _wcache.clear()
+        return
+    spans = [(p.data_ptr(), p.data_ptr() + p.numel() * p.element_size()) for p in params]
+
+    def ptr(k):
+        return k[1] if k[0] == "conv" else k[0]
+    for k in [k for k in _wcache if any(lo <= ptr(k) < hi for lo, hi in spans)]:
+        del _wcache[k]
+
+
+def _needs_grad(*ts):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+# ------------------------------------------------------------------------------------------
+# cast
+# ------------------------------------------------------------------------------------------
+class _Cast(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.src = x.dtype
+        return ops.cast(x, dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.cast(g, ctx.src), None
+
+
+def cast(x, dtype):
+    if x.dtype == dtype:
+        return x
+    if _needs_grad(x):
+        return _Cast.apply(x, dtype)
+    return ops.cast(x, dtype)
+
+
+def to_compute(x):
+    return cast(x, compute_dtype())
+
+
+# ------------------------------------------------------------------------------------------
+# linear: y = act(x W^T + b) + beta * resid
+# ------------------------------------------------------------------------------------------
+def _linear_bwd(x2, wc, dpre, need_dx, need_dw, need_db, dx_dtype):
+    """dpre [M, N] (compute dtype or f32) -> dx [M, K] (dx_dtype), dW [N, K] f32, db [N] f32."""
+    M, N = dpre.shape
+    K = x2.shape[1]
+    dx = dw = db = None
+    if need_db:
+        db = ops.colsum(dpre)
+    dpc = dpre if dpre.dtype == wc.dtype else ops.cast(dpre, wc.dtype)
+    if need_dx:
+        dx = torch.empty(M, K, device=dpre.device, dtype=dx_dtype)
+        ops.gemm_raw(dpc, wc, dx, m=M, n=K, k=N, layout_a=0, lda=dpc.stride(0), layout_b=1,
+                     ldb=wc.stride(0), ldc=K)
+    if need_dw:
+        xc = x2 if x2.dtype == wc.dtype else ops.cast(x2, wc.dtype)
+        dw = torch.empty(N, K, device=dpre.device, dtype=torch.float32)
+        ops.gemm_raw(dpc, xc, dw, m=N, n=K, k=M, layout_a=1, lda=dpc.stride(0), layout_b=1,
+                     ldb=xc.stride(0), ldc=K)
+    return dx, dw, db
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, resid, act, beta, out_dtype):
+        wc = wcast(w)
+        xc = x if x.dtype == wc.dtype else ops.cast(x, wc.dtype)
+        shp = x.shape
+        x2 = xc.reshape(-1, shp[-1])
+        N = w.shape[0]
+        aux = None
+        if act != L.ACT_NONE:
+            aux = torch.empty(x2.shape[0], N, device=x.device, dtype=out_dtype)
+        y = ops.linear(x2, wc, bias=b, act=act, resid=(resid.reshape(-1, N) if resid is not None else None),
+                       beta=beta, out_dtype=out_dtype, aux=aux)
+        ctx.save_for_backward(x2, w, aux)
+        ctx.act, ctx.beta, ctx.xdtype, ctx.shape = act, beta, x.dtype, shp
+        ctx.has_b, ctx.has_r = b is not None, resid is not None
+        return y.reshape(*shp[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, aux = ctx.saved_tensors
+        N = w.shape[0]
+        dy2 = dy.reshape(-1, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dpre = ops.act_bwd(ctx.act, aux, dy2, out_dtype=torch.float32) if ctx.act != L.ACT_NONE else dy2
+        wc = wcast(w)
+        dx, dw, db = _linear_bwd(x2, wc, dpre, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                 ctx.has_b and ctx.needs_input_grad[2], torch.float32)
+        if dx is not None:
+            dx = dx.reshape(ctx.shape)
+            if ctx.xdtype != torch.float32:
+                dx = ops.cast(dx, ctx.xdtype)
+        dres = None
+        if ctx.has_r and ctx.needs_input_grad[3]:
+            dres = dy if ctx.beta == 1.0 else dy * ctx.beta
+        return dx, dw, db, dres, None, None, None
+
+
+def linear(x, w, b=None, act=L.ACT_NONE, resid=None, beta=1.0, out_dtype=None):
+    """nn.Linear (+ fused activation / residual). Operands in the compute dtype, f32 accumulate."""
+    out_dtype = out_dtype or compute_dtype()
+    if _needs_grad(x, w, b, resid):
+        return _Linear.apply(x, w, b, resid, act, beta, out_dtype)
+    wc = wcast(w)
+    xc = x if x.dtype == wc.dtype else ops.cast(x, wc.dtype)
+    return ops.linear(xc, wc, bias=b, act=act, resid=resid, beta=beta, out_dtype=out_dtype)
+
+
+# ------------------------------------------------------------------------------------------
+# layernorm (f32 in / f32 out)
+# ------------------------------------------------------------------------------------------
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        y, mean, rstd = ops.layernorm(x, w, b, eps=eps, out_dtype=torch.float32, stats=True)
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.has_w, ctx.has_b = w is not None, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        C = x.shape[-1]
+        dw = torch.zeros(C, device=x.device) if ctx.has_w and ctx.needs_input_grad[1] else None
+        db = torch.zeros(C, device=x.device) if ctx.has_b and ctx.needs_input_grad[2] else None
+        dx = ops.layernorm_bwd(x, dy, mean, rstd, w, dw, db)
+        if x.dtype != torch.float32:
+            dx = ops.cast(dx, x.dtype)
+        return dx, dw, db, None
+
+
+def layer_norm(x, w=None, b=None, eps=1e-5):
+    if _needs_grad(x, w, b):
+        return _LayerNorm.apply(x, w, b, eps)
+    return ops.layernorm(x, w, b, eps=eps, out_dtype=torch.float32)
+
+
+# ------------------------------------------------------------------------------------------
+# multi-head attention core: o = softmax(q k^T * scale) v, per head
+# q [B, Lq, C], k/v [B, Lk, C] views with unit-stride last dim (may be slices of packed
+# projections). Backward is the materialised form on batched GEMMs.
+# ------------------------------------------------------------------------------------------
+def _attn_bwd(q, k, v, o, lse, do, heads, scale, dq, dk, dv):
+    """Materialised attention backward on batched GEMMs; dq/dk/dv are (possibly strided) views
+    [B, L, C] into the packed gradient buffers."""
+    B, Lq, C = q.shape
+    Lk = k.shape[1]
+    D = C // heads
+    dt = q.dtype
+    dev = q.device
+    BH = (B, heads)
+    sz = heads * Lq * Lk
+    S = torch.empty(B, heads, Lq, Lk, device=dev, dtype=torch.float32)
+    ops.gemm_raw(q, k, S, m=Lq, n=Lk, k=D, layout_a=0, lda=q.stride(1), layout_b=0, ldb=k.stride(1),
+                 ldc=Lk, batch=BH, stride_a=(q.stride(0), D), stride_b=(k.stride(0), D),
+                 stride_c=(sz, Lq * Lk))
+    P = torch.empty(B, heads, Lq, Lk, device=dev, dtype=dt)
+    rows = B * heads * Lq
+    L.check(L.load().comet_attn_probs(ops.dt(P), S.data_ptr(), lse.data_ptr(), P.data_ptr(), rows, Lk, Lk, Lk,
+                                      float(scale), ops.stream()), "attn_probs")
+    dP = S  # dP overwrites S
+    ops.gemm_raw(do, v, dP, m=Lq, n=Lk, k=D, layout_a=0, lda=do.stride(1), layout_b=0, ldb=v.stride(1),
+                 ldc=Lk, batch=BH, stride_a=(do.stride(0), D), stride_b=(v.stride(0), D),
+                 stride_c=(sz, Lq * Lk))
+    delta = torch.empty(B, heads, Lq, device=dev, dtype=torch.float32)
+    L.check(L.load().comet_attn_delta(ops.dt(o), do.data_ptr(), o.data_ptr(), delta.data_ptr(), B, heads, Lq, D,
+                                      o.stride(0), D, o.stride(1), do.stride(0), D, do.stride(1), ops.stream()),
+            "attn_delta")
+    dS = torch.empty(B, heads, Lq, Lk, device=dev, dtype=dt)
+    L.check(L.load().comet_attn_dsoftmax(ops.dt(P), P.data_ptr(), dP.data_ptr(), delta.data_ptr(), dS.data_ptr(),
+                                         rows, Lk, Lk, float(scale), ops.stream()), "attn_dsoftmax")
+    del S, dP
+    # dV = P^T dO
+    ops.gemm_raw(P, do, dv, m=Lk, n=D, k=Lq, layout_a=1, lda=Lk, layout_b=1, ldb=do.stride(1), ldc=dv.stride(1),
+                 batch=BH, stride_a=(sz, Lq * Lk), stride_b=(do.stride(0), D), stride_c=(dv.stride(0), D))
+    # dQ = dS K
+    ops.gemm_raw(dS, k, dq, m=Lq, n=D, k=Lk, layout_a=0, lda=Lk, layout_b=1, ldb=k.stride(1), ldc=dq.stride(1),
+                 batch=BH, stride_a=(sz, Lq * Lk), stride_b=(k.stride(0), D), stride_c=(dq.stride(0), D))
+    # dK = dS^T Q
+    ops.gemm_raw(dS, q, dk, m=Lk, n=D, k=Lq, layout_a=1, lda=Lk, layout_b=1, ldb=q.stride(1), ldc=dk.stride(1),
+                 batch=BH, stride_a=(sz, Lq * Lk), stride_b=(q.stride(0), D), stride_c=(dk.stride(0), D))
+
+
+def _split(qsrc, kvsrc, C):
+    if kvsrc is None:  # packed self-attention projections [B, L, 3C]
+        return qsrc[..., :C], qsrc[..., C:2 * C], qsrc[..., 2 * C:]
+    return qsrc, kvsrc[..., :C], kvsrc[..., C:]
+
+
+class _Attention(torch.autograd.Function):
+    """qsrc: packed [B, L, 3C] (self) or [B, Lq, C] (cross, with kvsrc [B, Lk, 2C])."""
+
+    @staticmethod
+    def forward(ctx, qsrc, kvsrc, heads, scale, C):
+        q, k, v = _split(qsrc, kvsrc, C)
+        o, lse = ops.attention(q, k, v, heads, scale, lse=True)
+        ctx.save_for_backward(qsrc, kvsrc, o, lse)
+        ctx.heads, ctx.scale, ctx.C = heads, scale, C
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qsrc, kvsrc, o, lse = ctx.saved_tensors
+        C = ctx.C
+        q, k, v = _split(qsrc, kvsrc, C)
+        do = do if do.dtype == q.dtype else ops.cast(do, q.dtype)
+        if not do.is_contiguous():
+            do = do.contiguous()
+        dqsrc = torch.empty_like(qsrc)
+        dkvsrc = None if kvsrc is None else torch.empty_like(kvsrc)
+        dq, dk, dv = _split(dqsrc, dkvsrc, C)
+        _attn_bwd(q, k, v, o, lse, do, ctx.heads, ctx.scale, dq, dk, dv)
+        return dqsrc, dkvsrc, None, None, None
+
+
+def attention(qsrc, kvsrc, heads, C, scale=None):
+    """softmax(q k^T * scale) v per head on packed projections (see _Attention)."""
+    scale = (C // heads) ** -0.5 if scale is None else scale
+    if _needs_grad(qsrc, kvsrc):
+        return _Attention.apply(qsrc, kvsrc, heads, scale, C)
+    q, k, v = _split(qsrc, kvsrc, C)
+    return ops.attention(q, k, v, heads, scale)
+
+
+# ------------------------------------------------------------------------------------------
+# small differentiable helpers of the camera head
+# ------------------------------------------------------------------------------------------
+class _LayerNormReLU(torch.autograd.Function):
+    """relu(LN_affine(x)) (TrajectoryEncoder, camera_predictor10.py:79-81)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        y, mean, rstd = ops.layernorm(x, w, b, eps=eps, out_dtype=torch.float32, stats=True, relu=True)
+        ctx.save_for_backward(x, w, mean, rstd, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, mean, rstd, y = ctx.saved_tensors
+        dpre = ops.act_bwd(L.ACT_RELU, y, dy.contiguous(), out_dtype=torch.float32)
+        C = x.shape[-1]
+        dw = torch.zeros(C, device=x.device) if ctx.needs_input_grad[1] else None
+        db = torch.zeros(C, device=x.device) if ctx.needs_input_grad[2] else None
+        dx = ops.layernorm_bwd(x, dpre, mean, rstd, w, dw, db) if (ctx.needs_input_grad[0] or dw is not None or db is not None) else None
+        return dx, dw, db, None
+
+
+def layer_norm_relu(x, w, b, eps=1e-5):
+    if _needs_grad(x, w, b):
+        return _LayerNormReLU.apply(x, w, b, eps)
+    return ops.layernorm(x, w, b, eps=eps, out_dtype=torch.float32, relu=True)
+
+
+class _RowScale(torch.autograd.Function):
+    """y[r, :] = x[r, :] * w[r] (confidence gating, camera_predictor10.py:332-333)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return ops.rowscale(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx, dw = ops.rowscale_bwd(x, w, dy, ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return dx, dw
+
+
+def rowscale(x, w):
+    """x [..., C], w [...] or [..., 1] (f32)."""
+    w = w.reshape(x.shape[:-1])
+    if _needs_grad(x, w):
+        return _RowScale.apply(x, w)
+    return ops.rowscale(x, w)
+
+
+class _Add(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b):
+        return ops.add(a, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, g
+
+
+def add(a, b):
+    if _needs_grad(a, b):
+        return _Add.apply(a, b)
+    return ops.add(a, b)
+
+
+class _AddRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, table, period):
+        return ops.add_rows(x, table, period, out_dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None, None
+
+
+def add_rows(x, table, period):
+    """x [..., C] + table[row % period] (constant positional / time embedding table)."""
+    if _needs_grad(x):
+        return _AddRows.apply(x, table, period)
+    return ops.add_rows(x, table, period, out_dtype=torch.float32)
+
+
+class _GAPR(torch.autograd.Function):
+    """Fused GAPR tail (camera_predictor10.py:385-460): quaternion F.normalize, pose loss vs the
+    GT encoding, frame-0 reset. Returns (pred_pose_enc [B*S, 7], losses [3])."""
+
+    @staticmethod
+    def forward(ctx, rot, uv, d, gt_enc, B, S, w_trans, w_rot):
+        rot2, uv2, d2 = rot.reshape(B * S, 4).contiguous(), uv.reshape(B * S, 2).contiguous(), d.reshape(B * S, 1).contiguous()
+        qn = torch.empty(B * S, 4, device=rot.device, dtype=torch.float32)
+        enc = torch.empty(B * S, 7, device=rot.device, dtype=torch.float32)
+        losses = torch.zeros(3, device=rot.device, dtype=torch.float32)
+        L.check(L.load().comet_gapr_fwd(rot2.data_ptr(), 4, uv2.data_ptr(), 2, d2.data_ptr(), 1,
+                                        None if gt_enc is None else gt_enc.data_ptr(), qn.data_ptr(), enc.data_ptr(),
+                                        losses.data_ptr(), B, S, float(w_trans), float(w_rot), ops.stream()), "gapr_fwd")
+        ctx.save_for_backward(rot2, uv2, d2, gt_enc, qn)
+        ctx.meta = (B, S, w_trans, w_rot, rot.shape, uv.shape, d.shape)
+        ctx.mark_non_differentiable(enc)
+        return enc, losses
+
+    @staticmethod
+    def backward(ctx, denc, dlosses):
+        rot2, uv2, d2, gt_enc, qn = ctx.saved_tensors
+        B, S, wt, wr, rs, us, ds = ctx.meta
+        if dlosses is None or gt_enc is None:
+            return None, None, None, None, None, None, None, None
+        dl = dlosses.contiguous().float()
+        drot = torch.empty(B * S, 4, device=rot2.device)
+        duv = torch.empty(B * S, 2, device=rot2.device)
+        dd = torch.empty(B * S, 1, device=rot2.device)
+        L.check(L.load().comet_gapr_bwd(rot2.data_ptr(), 4, uv2.data_ptr(), 2, d2.data_ptr(), 1, gt_enc.data_ptr(),
+                                        qn.data_ptr(), dl.data_ptr(), drot.data_ptr(), duv.data_ptr(), dd.data_ptr(),
+                                        B, S, float(wt), float(wr), ops.stream()), "gapr_bwd")
+        return drot.reshape(rs), duv.reshape(us), dd.reshape(ds), None, None, None, None, None
+
+
+def gapr(rot, uv, d, gt_enc, B, S, w_trans=1.0, w_rot=2.0):
+    """(pred_pose_enc [B*S, 7], losses [3] = (loss, loss_trans, loss_rot))."""
+    return _GAPR.apply(rot, uv, d, gt_enc, B, S, w_trans, w_rot)
+
+
+class _Harmonic(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, diag_cov, freqs, append):
+        ctx.save_for_backward(x, diag_cov, freqs)
+        ctx.append = append
+        return ops.harmonic_fwd(x, freqs, append, diag_cov)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, cov, freqs = ctx.saved_tensors
+        dx, dcov = ops.harmonic_bwd(x, freqs, ctx.append, dy, cov)
+        return dx, (dcov if ctx.needs_input_grad[1] else None), None, None
+
+
+def harmonic(x, freqs, append_input, diag_cov=None):
+    if _needs_grad(x, diag_cov):
+        return _Harmonic.apply(x, diag_cov, freqs, append_input)
+    return ops.harmonic_fwd(x, freqs, append_input, diag_cov)
+
+
+def wcast_conv(w, k_align=8):
+    """Conv weight [Cout, Cin, kh, kw] -> GEMM operand [Cout, Kpad] in the compute dtype, column
+    order (ky, kx, ci) matching comet_im2col_nhwc, K padded with zeros to k_align (cached)."""
+    dt = compute_dtype()
+    key = ("conv", w.data_ptr(), tuple(w.shape), dt)
+    hit = _wcache.get(key)
+    if hit is not None:
+        return hit
+    cout, cin, kh, kw = w.shape
+    K = cin * kh * kw
+    Kp = (K + k_align - 1) // k_align * k_align
+    wm = torch.zeros(cout, Kp, device=w.device, dtype=dt)
+    wm[:, :K] = w.detach().permute(0, 2, 3, 1).reshape(cout, K).to(dt)
+    _wcache[key] = wm
+    return wm

@@ -1,0 +1,128 @@
+"""Transformer / CNN building blocks of the COMET hot path (mirror of comet/models/modules.py).
+
+Parameter names and shapes match the reference exactly (state_dict drop-in); forward and
+backward run through comet_amd.functional (libcomet_hip.so). Residual streams are f32.
+
+  Mlp            modules.py:119-154   fc1 -> GELU(erf) -> fc2
+  AttnBlock      modules.py:248-295   x = LN(x); x = x + MHA(x); x = x + Mlp(LN(x))
+  CrossAttnBlock modules.py:298-344   same with ctx = LN_affine(ctx, eps 1e-5)
+  ResidualBlock  modules.py:39-116    conv3x3-IN-ReLU x2 (+ 1x1 s2 downsample), NHWC
+"""
+import torch
+import torch.nn as nn
+
+from .. import _lib as L
+from .. import functional as F
+from .. import ops
+
+
+class Mlp(nn.Module):
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU,
+                 norm_layer=None, bias=True, drop=0.0, use_conv=False):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        self.fc1 = nn.Linear(in_features, hidden_features, bias=bias)
+        self.act = act_layer()
+        self.drop1 = nn.Dropout(drop)
+        self.fc2 = nn.Linear(hidden_features, out_features, bias=bias)
+        self.drop2 = nn.Dropout(drop)
+
+    def forward(self, x, resid=None, out_dtype=torch.float32):
+        h = F.linear(x, self.fc1.weight, self.fc1.bias, act=L.ACT_GELU)
+        return F.linear(h, self.fc2.weight, self.fc2.bias, resid=resid, out_dtype=out_dtype)
+
+
+def _mha_holder(C, heads):
+    """nn.MultiheadAttention used only as the parameter container (in_proj_weight [3C, C],
+    in_proj_bias, out_proj.{weight,bias}) so checkpoints load unchanged."""
+    return nn.MultiheadAttention(embed_dim=C, num_heads=heads, batch_first=True)
+
+
+class AttnBlock(nn.Module):
+    def __init__(self, hidden_size, num_heads, attn_class=nn.MultiheadAttention, mlp_ratio=4.0, **kw):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(hidden_size, elementwise_affine=False, eps=1e-6)
+        self.norm2 = nn.LayerNorm(hidden_size, elementwise_affine=False, eps=1e-6)
+        self.attn = _mha_holder(hidden_size, num_heads)
+        self.mlp = Mlp(in_features=hidden_size, hidden_features=int(hidden_size * mlp_ratio), drop=0)
+        self.heads = num_heads
+
+    def forward(self, x, mask=None):
+        C = x.shape[-1]
+        a = self.attn
+        x = F.layer_norm(x, eps=1e-6)
+        qkv = F.linear(x, a.in_proj_weight, a.in_proj_bias)
+        o = F.attention(qkv, None, self.heads, C)
+        x = F.linear(o, a.out_proj.weight, a.out_proj.bias, resid=x, out_dtype=torch.float32)
+        return self.mlp(F.layer_norm(x, eps=1e-6), resid=x)
+
+
+class CrossAttnBlock(nn.Module):
+    def __init__(self, hidden_size, context_dim, num_heads=1, mlp_ratio=4.0, **kw):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(hidden_size, elementwise_affine=False, eps=1e-6)
+        self.norm_context = nn.LayerNorm(hidden_size)
+        self.norm2 = nn.LayerNorm(hidden_size, elementwise_affine=False, eps=1e-6)
+        self.cross_attn = _mha_holder(hidden_size, num_heads)
+        self.mlp = Mlp(in_features=hidden_size, hidden_features=int(hidden_size * mlp_ratio), drop=0)
+        self.heads = num_heads
+
+    def forward(self, x, context, mask=None):
+        C = x.shape[-1]
+        a = self.cross_attn
+        x = F.layer_norm(x, eps=1e-6)
+        ctx = F.layer_norm(context, self.norm_context.weight, self.norm_context.bias, eps=1e-5)
+        W, b = a.in_proj_weight, a.in_proj_bias
+        q = F.linear(x, W[:C], b[:C])
+        kv = F.linear(ctx, W[C:], b[C:])
+        o = F.attention(q, kv, self.heads, C)
+        x = F.linear(o, a.out_proj.weight, a.out_proj.bias, resid=x, out_dtype=torch.float32)
+        return self.mlp(F.layer_norm(x, eps=1e-6), resid=x)
+
+
+# ------------------------------------------------------------------------------------------
+# CNN blocks (no-grad, NHWC activations in the compute dtype)
+# ------------------------------------------------------------------------------------------
+def conv2d_nhwc(x, conv, stride, pad, out_dtype=None):
+    """nn.Conv2d on NHWC x via im2col + MFMA GEMM. conv.weight [Cout, Cin, kh, kw]."""
+    w = conv.weight
+    cout, cin, kh, kw = w.shape
+    wm = F.wcast_conv(w)
+    if kh == 1 and kw == 1 and stride == 1 and pad == 0:
+        n, h, wd, c = x.shape
+        y = F.linear(x.reshape(-1, c), wm, conv.bias, out_dtype=out_dtype)
+        return y.reshape(n, h, wd, cout)
+    xc = x if x.dtype == wm.dtype else ops.cast(x, wm.dtype)
+    cols, oh, ow = ops.im2col_nhwc(xc, kh, kw, stride, pad, out_dtype=wm.dtype, ldc=wm.shape[1])
+    y = F.linear(cols, wm, conv.bias, out_dtype=out_dtype)
+    return y.reshape(x.shape[0], oh, ow, cout)
+
+
+class ResidualBlock(nn.Module):
+    def __init__(self, in_planes, planes, norm_fn="group", stride=1, kernel_size=3):
+        super().__init__()
+        if norm_fn != "instance":
+            raise NotImplementedError("the COMET path only uses norm_fn='instance'")
+        self.conv1 = nn.Conv2d(in_planes, planes, kernel_size=kernel_size, padding=1, stride=stride)
+        self.conv2 = nn.Conv2d(planes, planes, kernel_size=kernel_size, padding=1)
+        self.relu = nn.ReLU(inplace=True)
+        self.norm1 = nn.InstanceNorm2d(planes)
+        self.norm2 = nn.InstanceNorm2d(planes)
+        self.stride = stride
+        if stride != 1:
+            self.norm3 = nn.InstanceNorm2d(planes)
+            self.downsample = nn.Sequential(nn.Conv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm3)
+        else:
+            self.downsample = None
+
+    def forward(self, x):
+        """x NHWC -> relu(x' + relu(IN(conv2(relu(IN(conv1(x)))))))."""
+        y = ops.instnorm_nhwc(conv2d_nhwc(x, self.conv1, self.stride, 1), relu=True)
+        y = conv2d_nhwc(y, self.conv2, 1, 1)
+        if self.downsample is not None:
+            xd = ops.instnorm_nhwc(conv2d_nhwc(x, self.downsample[0], self.stride, 0))
+        else:
+            xd = x
+        # relu(x' + relu(IN(y))) in one pass
+        return ops.instnorm_nhwc(y, res=xd, relu=True, relu_inner=True)

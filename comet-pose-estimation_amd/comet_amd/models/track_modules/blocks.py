@@ -1,0 +1,155 @@
+"""Tracker building blocks (mirror of comet/models/track_modules/blocks.py) on libcomet_hip.so.
+
+The tracker is frozen and always runs under no_grad (E2Epose2.py:176), so these modules are
+forward-only. Activations are channels-last (NHWC) in the compute dtype; convolutions are
+im2col + MFMA GEMM, InstanceNorm/ReLU/residual tails are fused kernels.
+
+  BasicEncoder   blocks.py:27-111   coarse feature net -> [B*S, H/8, W/8, 128]
+  ShallowEncoder blocks.py:114-196  fine patch feature net -> [n, 31, 31, 32]
+  EfficientUpdateFormer blocks.py:205-348 (time / virtual-track space attention)
+"""
+import torch
+import torch.nn as nn
+
+from ... import functional as F
+from ... import ops
+from ..modules import AttnBlock, CrossAttnBlock, ResidualBlock, conv2d_nhwc
+
+
+class BasicEncoder(nn.Module):
+    def __init__(self, input_dim=3, output_dim=128, stride=4, use_trans=False, cfg=None):
+        super().__init__()
+        self.stride = stride
+        self.norm_fn = "instance"
+        self.in_planes = output_dim // 2
+        self.norm1 = nn.InstanceNorm2d(self.in_planes)
+        self.norm2 = nn.InstanceNorm2d(output_dim * 2)
+        self.conv1 = nn.Conv2d(input_dim, self.in_planes, kernel_size=7, stride=2, padding=3)
+        self.relu1 = nn.ReLU(inplace=True)
+        self.layer1 = self._make_layer(output_dim // 2, stride=1)
+        self.layer2 = self._make_layer(output_dim // 4 * 3, stride=2)
+        self.layer3 = self._make_layer(output_dim, stride=2)
+        self.layer4 = self._make_layer(output_dim, stride=2)
+        self.conv2 = nn.Conv2d(output_dim * 3 + output_dim // 4, output_dim * 2, kernel_size=3, padding=1)
+        self.relu2 = nn.ReLU(inplace=True)
+        self.conv3 = nn.Conv2d(output_dim * 2, output_dim, kernel_size=1)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    def _make_layer(self, dim, stride=1):
+        layer1 = ResidualBlock(self.in_planes, dim, self.norm_fn, stride=stride)
+        layer2 = ResidualBlock(dim, dim, self.norm_fn, stride=1)
+        self.in_planes = dim
+        return nn.Sequential(layer1, layer2)
+
+    @torch.no_grad()
+    def forward(self, x, H, W):
+        """x NHWC [n, H, W, 3] (compute dtype) -> fmaps NHWC [n, H/stride, W/stride, 128]."""
+        x = ops.instnorm_nhwc(conv2d_nhwc(x, self.conv1, 2, 3), relu=True)
+        a = self.layer1(x)
+        b = self.layer2(a)
+        c = self.layer3(b)
+        d = self.layer4(c)
+        oh, ow = H // self.stride, W // self.stride
+        ups = [ops.resize_bilinear(t, oh, ow, nhwc=True) for t in (a, b, c, d)]
+        x = torch.cat(ups, dim=-1)
+        x = ops.instnorm_nhwc(conv2d_nhwc(x, self.conv2, 1, 1), relu=True)
+        return conv2d_nhwc(x, self.conv3, 1, 0)
+
+
+class ShallowEncoder(nn.Module):
+    def __init__(self, input_dim=3, output_dim=32, stride=1, norm_fn="instance", cfg=None):
+        super().__init__()
+        self.stride = stride
+        self.norm_fn = norm_fn
+        self.in_planes = output_dim
+        self.norm1 = nn.InstanceNorm2d(self.in_planes)
+        self.norm2 = nn.InstanceNorm2d(output_dim * 2)
+        self.conv1 = nn.Conv2d(input_dim, self.in_planes, kernel_size=3, stride=2, padding=1)
+        self.relu1 = nn.ReLU(inplace=True)
+        self.layer1 = self._make_layer(output_dim, stride=2)
+        self.layer2 = self._make_layer(output_dim, stride=2)
+        self.conv2 = nn.Conv2d(output_dim, output_dim, kernel_size=1)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    def _make_layer(self, dim, stride=1):
+        self.in_planes = dim
+        return ResidualBlock(self.in_planes, dim, self.norm_fn, stride=stride)
+
+    @torch.no_grad()
+    def forward(self, x):
+        """x NHWC [n, P, P, 3] -> NHWC [n, P/stride, P/stride, 32]."""
+        _, H, W, _ = x.shape
+        x = ops.instnorm_nhwc(conv2d_nhwc(x, self.conv1, 2, 1), relu=True)
+        h, w = x.shape[1], x.shape[2]
+        tmp = self.layer1(x)
+        x = ops.resize_bilinear(tmp, h, w, nhwc=True, out=x, add=True)
+        tmp = self.layer2(tmp)
+        x = ops.resize_bilinear(tmp, h, w, nhwc=True, out=x, add=True)
+        n, _, _, c = x.shape
+        x = F.linear(x.reshape(-1, c), F.wcast(self.conv2.weight.reshape(c, c)), self.conv2.bias,
+                     resid=x.reshape(-1, c), out_dtype=x.dtype).reshape(n, h, w, c)
+        return ops.resize_bilinear(x, H // self.stride, W // self.stride, nhwc=True)
+
+
+class EfficientUpdateFormer(nn.Module):
+    def __init__(self, space_depth=6, time_depth=6, input_dim=320, hidden_size=384, num_heads=8, output_dim=130,
+                 mlp_ratio=4.0, add_space_attn=True, num_virtual_tracks=64):
+        super().__init__()
+        self.out_channels = 2
+        self.num_heads = num_heads
+        self.hidden_size = hidden_size
+        self.add_space_attn = add_space_attn
+        self.input_transform = torch.nn.Linear(input_dim, hidden_size, bias=True)
+        self.flow_head = torch.nn.Linear(hidden_size, output_dim, bias=True)
+        self.num_virtual_tracks = num_virtual_tracks
+        self.virual_tracks = nn.Parameter(torch.randn(1, num_virtual_tracks, 1, hidden_size)) if add_space_attn else None
+        self.time_blocks = nn.ModuleList([AttnBlock(hidden_size, num_heads, mlp_ratio=mlp_ratio) for _ in range(time_depth)])
+        if add_space_attn:
+            self.space_virtual_blocks = nn.ModuleList(
+                [AttnBlock(hidden_size, num_heads, mlp_ratio=mlp_ratio) for _ in range(space_depth)])
+            self.space_point2virtual_blocks = nn.ModuleList(
+                [CrossAttnBlock(hidden_size, hidden_size, num_heads, mlp_ratio=mlp_ratio) for _ in range(space_depth)])
+            self.space_virtual2point_blocks = nn.ModuleList(
+                [CrossAttnBlock(hidden_size, hidden_size, num_heads, mlp_ratio=mlp_ratio) for _ in range(space_depth)])
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                torch.nn.init.xavier_uniform_(m.weight)
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+
+    @torch.no_grad()
+    def forward(self, input_tensor, mask=None):
+        """input [B, N, T, Din] (compute dtype) -> [B, N, T, Dout] f32."""
+        B, N0, T, _ = input_tensor.shape
+        init = F.linear(input_tensor, self.input_transform.weight, self.input_transform.bias, out_dtype=torch.float32)
+        tokens = init
+        if self.add_space_attn:
+            vt = self.virual_tracks.detach().float().expand(B, -1, T, -1)
+            tokens = torch.cat([tokens, vt], dim=1)
+        N = tokens.shape[1]
+        C = self.hidden_size
+        j = 0
+        space_every = len(self.time_blocks) // len(self.space_virtual_blocks) if self.add_space_attn else 0
+        for i in range(len(self.time_blocks)):
+            tokens = self.time_blocks[i](tokens.reshape(B * N, T, C)).reshape(B, N, T, C)
+            if self.add_space_attn and i % space_every == 0:
+                st = tokens.permute(0, 2, 1, 3).reshape(B * T, N, C)
+                pt = st[:, :N - self.num_virtual_tracks]
+                vt = st[:, N - self.num_virtual_tracks:]
+                vt = self.space_virtual2point_blocks[j](vt, pt)
+                vt = self.space_virtual_blocks[j](vt)
+                pt = self.space_point2virtual_blocks[j](pt, vt)
+                tokens = torch.cat([pt, vt], dim=1).reshape(B, T, N, C).permute(0, 2, 1, 3).contiguous()
+                j += 1
+        if self.add_space_attn:
+            tokens = tokens[:, :N - self.num_virtual_tracks]
+        return _flow(tokens, init, self.flow_head)
+
+
+def _flow(tokens, init, head):
+    x = ops.add(tokens.contiguous(), init)
+    return F.linear(x, head.weight, head.bias, out_dtype=torch.float32)

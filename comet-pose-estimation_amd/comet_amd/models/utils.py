@@ -1,0 +1,58 @@
+"""Camera containers and constants of the COMET path (mirror of the pieces of
+comet/models/utils.py and train_eval_func_new_cp5.py the path touches)."""
+import torch
+
+# pose_encoding_to_camera2 intrinsics per dataset (utils.py:352-371): (fx, fy, cx, cy)
+INTRINSICS = {
+    "spark": (1744.92206139719, 1746.58640701753, 737.272795902663, 528.471960188736),
+    "AMD": (268.44444444, 268.44444444, 320.0, 240.0),
+    "AMD_eval": (268.44444444, 268.44444444, 320.0, 240.0),
+    "AMD_test": (214.75555555, 286.34074074, 256.0, 256.0),
+}
+
+
+class QuaternionCameras:
+    """train_eval_func_new_cp5.py:21-79: R (N,4) w x y z, T_uvz (N,3), T (N,3), focal (N,2),
+    principal point (N,2), ratio (collated float64 tensor or float)."""
+
+    def __init__(self, R, T_uvz, T, focal_length=1.0, principal_point=None, ratio=None, device="cpu"):
+        self.device = device
+        self.R = R.to(device)
+        self.T = T.to(device)
+        self.T_uvz = T_uvz.to(device)
+        self.ratio = ratio
+        N = self.R.shape[0]
+        if isinstance(focal_length, (float, int)):
+            self.focal_length = torch.full((N, 2), float(focal_length), device=device)
+        else:
+            fl = focal_length.to(device)
+            if fl.dim() == 0:
+                self.focal_length = fl.expand(N, 2)
+            elif fl.dim() == 1:
+                self.focal_length = fl.view(-1, 1).expand(-1, 2)
+            else:
+                self.focal_length = fl
+        if principal_point is None:
+            self.principal_point = torch.zeros((N, 2), device=device)
+        else:
+            pp = torch.as_tensor(principal_point, dtype=torch.float32, device=device)
+            self.principal_point = pp.expand(N, 2) if pp.dim() == 1 else pp
+
+
+class PredCameras:
+    """Output cameras of pose_encoding_to_camera2 (R quaternion, T float64, focal [N, 0])."""
+
+    def __init__(self, R, T, focal_length):
+        self.R = R
+        self.T = T
+        self.focal_length = focal_length
+        self.device = R.device
+
+    def get_world_to_view_transform(self):
+        from ..minipytorch3d.rotation_conversions import quaternion_to_matrix
+        Rm = quaternion_to_matrix(self.R)
+        M = torch.zeros(self.R.shape[0], 4, 4, dtype=Rm.dtype, device=Rm.device)
+        M[:, :3, :3] = Rm
+        M[:, 3, :3] = self.T.to(Rm.dtype)
+        M[:, 3, 3] = 1.0
+        return M

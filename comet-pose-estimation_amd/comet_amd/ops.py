@@ -102,18 +102,47 @@ def linear(x, w, bias=None, act=L.ACT_NONE, resid=None, out=None, out_dtype=None
 # ------------------------------------------------------------------------------------------
 # LayerNorm
 # ------------------------------------------------------------------------------------------
-def layernorm(x, weight=None, bias=None, eps=1e-5, out_dtype=None, stats=False, out=None):
+def _rows2d(x):
+    """(rows, row stride) of a tensor whose last dim is unit-stride and whose leading dims
+    collapse to a single uniform row stride; None if they do not."""
+    if x.stride(-1) != 1:
+        return None
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if x.dim() == 1:
+        return rows, C
+    lead = [(s, st) for s, st in zip(x.shape[:-1], x.stride()[:-1]) if s != 1]
+    if not lead:
+        return rows, C
+    ld = lead[-1][1]
+    expect = ld
+    for s, st in reversed(lead):
+        if st != expect:
+            return None
+        expect = st * s
+    return rows, ld
+
+
+def layernorm(x, weight=None, bias=None, eps=1e-5, out_dtype=None, stats=False, out=None, relu=False):
     _req_cuda(x)
     C = x.shape[-1]
-    xc = x if x.is_contiguous() else x.contiguous()
-    rows = xc.numel() // C
+    r = _rows2d(x)
+    xc = x
+    if r is None:
+        xc = x.contiguous()
+        r = _rows2d(xc)
+    rows, ldx = r
     y = out if out is not None else torch.empty(x.shape, device=x.device, dtype=out_dtype or x.dtype)
+    ry = _rows2d(y)
+    if ry is None:
+        raise L.CometHipError("layernorm: output rows must be uniformly strided")
     mean = rstd = None
     if stats:
         mean = torch.empty(rows, device=x.device, dtype=torch.float32)
         rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
     L.check(L.load().comet_layernorm_fwd(dt(xc), dt(y), _p(xc), _p(weight), _p(bias), _p(y), _p(mean),
-                                         _p(rstd), rows, C, float(eps), stream()), "layernorm")
+                                         _p(rstd), rows, C, ldx, ry[1], float(eps), int(relu), stream()),
+            "layernorm")
     if stats:
         return y, mean, rstd
     return y
@@ -197,18 +226,16 @@ def im2col_nhwc(x, kh, kw, stride, pad, out_dtype=None, ldc=None):
     kk = kh * kw * c
     ldc = ldc or kk
     cols = torch.empty(n * oh * ow, ldc, device=x.device, dtype=out_dtype or x.dtype)
-    if ldc != kk:
-        cols[:, kk:].zero_()
     L.check(L.load().comet_im2col_nhwc(dt(x), dt(cols), _p(x), _p(cols), n, h, w, c, kh, kw, stride, pad,
                                        oh, ow, ldc, stream()), "im2col")
     return cols, oh, ow
 
 
-def instnorm_nhwc(x, res=None, relu=False, eps=1e-5, out=None):
+def instnorm_nhwc(x, res=None, relu=False, eps=1e-5, out=None, relu_inner=False):
     n, h, w, c = x.shape
     out = out if out is not None else torch.empty_like(x)
     L.check(L.load().comet_instnorm_nhwc(dt(x), _p(x), _p(res), _p(out), n, h * w, c, float(eps),
-                                         int(relu), 0, stream()), "instnorm")
+                                         int(relu), int(relu_inner), stream()), "instnorm")
     return out
 
 
@@ -226,3 +253,212 @@ def resize_bilinear(x, oh, ow, nhwc, out=None, add=False, out_dtype=None):
     L.check(L.load().comet_resize_bilinear(dt(xc), dt(out), int(nhwc), _p(xc), _p(out), n, c, h, w, oh, ow,
                                            int(add), stream()), "resize_bilinear")
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# camera head helpers
+# ------------------------------------------------------------------------------------------
+def _chk(rc, what):
+    L.check(rc, what)
+
+
+def act_fwd(act, x, out_dtype=None):
+    xc = x.contiguous()
+    y = torch.empty(x.shape, device=x.device, dtype=out_dtype or x.dtype)
+    _chk(L.load().comet_act_fwd(act, dt(xc), dt(y), _p(xc), _p(y), xc.numel(), stream()), "act_fwd")
+    return y
+
+
+def binary(op, a, b, out=None):
+    a = a.contiguous()
+    b = b.contiguous()
+    out = out if out is not None else torch.empty_like(a)
+    _chk(L.load().comet_binary(op, dt(a), _p(a), _p(b), _p(out), a.numel(), stream()), "binary")
+    return out
+
+
+def add_relu(a, b):
+    return binary(1, a, b)
+
+
+def add(a, b, out=None):
+    return binary(0, a, b, out)
+
+
+def add_rows(x, table, period, out_dtype=None, out=None):
+    """x [..., C] (+ table[(row % period), :]); table f32 [period, C]."""
+    C = x.shape[-1]
+    r = _rows2d(x)
+    xc = x
+    if r is None:
+        xc = x.contiguous()
+        r = _rows2d(xc)
+    rows, ldx = r
+    y = out if out is not None else torch.empty(x.shape, device=x.device, dtype=out_dtype or x.dtype)
+    ry = _rows2d(y)
+    _chk(L.load().comet_add_rows(dt(xc), dt(y), _p(xc), _p(table), _p(y), rows, C, period, ldx, ry[1], stream()),
+         "add_rows")
+    return y
+
+
+def rowscale(x, w):
+    xc = x.contiguous()
+    C = x.shape[-1]
+    y = torch.empty_like(xc)
+    _chk(L.load().comet_rowscale_fwd(dt(xc), _p(xc), _p(w), _p(y), xc.numel() // C, C, stream()), "rowscale")
+    return y
+
+
+def rowscale_bwd(x, w, dy, need_dx=True, need_dw=True):
+    xc = x.contiguous()
+    C = x.shape[-1]
+    rows = xc.numel() // C
+    dyc = dy.contiguous().float() if dy.dtype != torch.float32 else dy.contiguous()
+    dx = torch.empty(x.shape, device=x.device, dtype=torch.float32) if need_dx else None
+    dw = torch.empty(w.shape, device=x.device, dtype=torch.float32) if need_dw else None
+    _chk(L.load().comet_rowscale_bwd(dt(xc), _p(xc), _p(w), _p(dyc), _p(dx), _p(dw), rows, C, stream()),
+         "rowscale_bwd")
+    return dx, dw
+
+
+def sincos_table(pos, dim, out=None, col0=0):
+    """get_1d_sincos_pos_embed_from_grid(dim, pos) on device -> [len(pos), dim] f32."""
+    pos = pos.contiguous().float()
+    m = pos.numel()
+    if out is None:
+        out = torch.empty(m, dim, device=pos.device, dtype=torch.float32)
+    _chk(L.load().comet_sincos_table(_p(pos), _p(out), m, dim, out.stride(0), col0, stream()), "sincos")
+    return out
+
+
+def sincos_2d(embed_dim, gh, gw, device):
+    """get_2d_sincos_pos_embed(embed_dim, (gh, gw)) as a [gh*gw, embed_dim] row table (row =
+    y*gw + x; first half encodes x (column), second half y (row): utils.py:724-804)."""
+    xs = torch.arange(gw, device=device, dtype=torch.float32).repeat(gh)
+    ys = torch.arange(gh, device=device, dtype=torch.float32).repeat_interleave(gw)
+    out = torch.empty(gh * gw, embed_dim, device=device, dtype=torch.float32)
+    sincos_table(xs, embed_dim // 2, out=out, col0=0)
+    sincos_table(ys, embed_dim // 2, out=out, col0=embed_dim // 2)
+    return out
+
+
+def pose_encode(R, T_uvz, focal, ratio, B, S):
+    enc = torch.empty(B * S, 8, device=R.device, dtype=torch.float32)
+    _chk(L.load().comet_pose_encode(_p(R.contiguous()), _p(T_uvz.contiguous()), _p(focal.contiguous()),
+                                    float(ratio), _p(enc), B, S, stream()), "pose_encode")
+    return enc
+
+
+def pose_decode(enc, R_gt, T_gt, ratio, intr, B, S):
+    Rout = torch.empty(B * S, 4, device=enc.device, dtype=torch.float32)
+    Tout = torch.empty(B * S, 3, device=enc.device, dtype=torch.float64)
+    fx, fy, cx, cy = intr
+    _chk(L.load().comet_pose_decode(_p(enc.contiguous()), _p(R_gt.contiguous()), _p(T_gt.contiguous()), float(ratio),
+                                    fx, fy, cx, cy, _p(Rout), _p(Tout), B, S, stream()), "pose_decode")
+    return Rout, Tout
+
+
+# ------------------------------------------------------------------------------------------
+# tracker
+# ------------------------------------------------------------------------------------------
+def sample_bilinear(fmap_nhwc, coords, border=True, out=None):
+    """fmap [B, H, W, C], coords [B, R, 2] (pixel x, y) -> [B, R, C] f32."""
+    B, H, W, C = fmap_nhwc.shape
+    R = coords.shape[1]
+    cc = coords.contiguous().float()
+    if out is None:
+        out = torch.empty(B, R, C, device=coords.device, dtype=torch.float32)
+    _chk(L.load().comet_sample_bilinear(dt(fmap_nhwc), _p(fmap_nhwc), fmap_nhwc.stride(0), H, W, C, _p(cc),
+                                        cc.stride(0), cc.stride(1), _p(out), out.stride(0), out.stride(1), B, R,
+                                        int(border), stream()), "sample_bilinear")
+    return out
+
+
+def corr_sample(pyramid, radius, feats, coords, out, col0, B, N, S):
+    C = pyramid[0].shape[-1]
+    levels = len(pyramid)
+    ptrs = (ctypes.c_void_p * levels)(*[p.data_ptr() for p in pyramid])
+    hs = (ctypes.c_int * levels)(*[p.shape[1] for p in pyramid])
+    ws = (ctypes.c_int * levels)(*[p.shape[2] for p in pyramid])
+    _chk(L.load().comet_corr_sample(dt(pyramid[0]), dt(feats), ptrs, hs, ws, levels, radius, C, _p(feats), _p(coords),
+                                    _p(out), out.stride(0), col0, B, N, S, stream()), "corr_sample")
+
+
+def tracker_tokens(coords, feats, latent, corr, corrdim, pos, tdim, x, rows, S):
+    _chk(L.load().comet_tracker_tokens(dt(x), _p(coords), _p(feats), latent, _p(corr), corr.stride(0), corrdim,
+                                       _p(pos), tdim, _p(x), rows, S, stream()), "tracker_tokens")
+
+
+def coords_update(coords, delta, preds, scale, B, N, S):
+    _chk(L.load().comet_coords_update(dt(delta), _p(coords), _p(delta), delta.stride(0), _p(preds), float(scale),
+                                      B, N, S, stream()), "coords_update")
+
+
+def avgpool2_nhwc(x):
+    n, H, W, C = x.shape
+    y = torch.empty(n, H // 2, W // 2, C, device=x.device, dtype=x.dtype)
+    _chk(L.load().comet_avgpool2_nhwc(dt(x), _p(x), _p(y), n, H, W, C, stream()), "avgpool2")
+    return y
+
+
+def patch_gather(images, coarse, pradius, out_dtype):
+    B, S, _, H, W = images.shape
+    N = coarse.shape[2]
+    P = 2 * pradius + 1
+    patches = torch.empty(B * S * N, P, P, 3, device=images.device, dtype=out_dtype)
+    topleft = torch.empty(B, S, N, 2, device=images.device, dtype=torch.int32)
+    query = torch.empty(B * N, 2, device=images.device, dtype=torch.float32)
+    _chk(L.load().comet_patch_gather(dt(patches), _p(images.contiguous()), _p(coarse.contiguous()), _p(patches),
+                                     _p(topleft), _p(query), B, S, N, H, W, pradius, stream()), "patch_gather")
+    return patches, topleft, query
+
+
+def refine_combine(fine, topleft, coarse, B, S, N):
+    refined = torch.empty(B, S, N, 2, device=fine.device, dtype=torch.float32)
+    _chk(L.load().comet_refine_combine(_p(fine), _p(topleft), _p(coarse.contiguous()), _p(refined), B, S, N, stream()),
+         "refine_combine")
+    return refined
+
+
+def track_score(qfeat, pfeat, fine, B, S, N, sradius=2):
+    P, C = pfeat.shape[-2], pfeat.shape[-1]
+    score = torch.empty(B, S, N, device=qfeat.device, dtype=torch.float32)
+    inv = torch.empty(B, S, N, device=qfeat.device, dtype=torch.float32)
+    _chk(L.load().comet_track_score(dt(pfeat), _p(qfeat.contiguous()), _p(pfeat), _p(fine.contiguous()), _p(score),
+                                    _p(inv), B, S, N, P, C, sradius, stream()), "track_score")
+    return score, inv
+
+
+def dino_prep(images_flat, R, patch, ldc, mean3, std3, out_dtype):
+    BS, _, H, W = images_flat.shape
+    g = R // patch
+    cols = torch.empty(BS * g * g, ldc, device=images_flat.device, dtype=out_dtype)
+    _chk(L.load().comet_dino_prep(dt(cols), _p(images_flat.contiguous()), _p(cols), BS, H, W, R, patch, ldc,
+                                  _p(mean3), _p(std3), stream()), "dino_prep")
+    return cols
+
+
+def harmonic_fwd(x, freqs, append_input, diag_cov=None):
+    dim = x.shape[-1]
+    n = freqs.numel()
+    rows = x.numel() // dim
+    xc = x.contiguous().float()
+    cov = diag_cov.contiguous().float() if diag_cov is not None else None
+    y = torch.empty(*x.shape[:-1], dim * (2 * n + int(append_input)), device=x.device, dtype=torch.float32)
+    _chk(L.load().comet_harmonic_fwd(_p(xc), _p(cov), _p(freqs), _p(y), rows, dim, n, int(append_input), stream()),
+         "harmonic_fwd")
+    return y
+
+
+def harmonic_bwd(x, freqs, append_input, dy, diag_cov=None):
+    dim = x.shape[-1]
+    n = freqs.numel()
+    rows = x.numel() // dim
+    xc = x.contiguous().float()
+    cov = diag_cov.contiguous().float() if diag_cov is not None else None
+    dyc = dy.contiguous().float()
+    dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+    dcov = torch.empty(x.shape, device=x.device, dtype=torch.float32) if cov is not None else None
+    _chk(L.load().comet_harmonic_bwd(_p(xc), _p(cov), _p(freqs), _p(dyc), _p(dx), _p(dcov), rows, dim, n,
+                                     int(append_input), stream()), "harmonic_bwd")
+    return dx, dcov

@@ -259,14 +259,14 @@ int dispatch_d(const comet_attn_args& a, hipStream_t s) {
 
 // ---- materialised backward helpers ----
 template <typename T>
-__global__ void probs_kernel(const T* __restrict__ S, const float* __restrict__ lse,
+__global__ void probs_kernel(const float* __restrict__ S, const float* __restrict__ lse,
                              T* __restrict__ P, int64_t rows, int64_t cols, int64_t lds,
                              int64_t ldp, float scale) {
   const int64_t r = blockIdx.y * (int64_t)gridDim.z + blockIdx.z;
   if (r >= rows) return;
   const float l = lse[r];
   for (int64_t c = blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256)
-    P[r * ldp + c] = from_f32<T>(__expf(to_f32(S[r * lds + c]) * scale - l));
+    P[r * ldp + c] = from_f32<T>(__expf(S[r * lds + c] * scale - l));
 }
 
 template <typename T>
@@ -287,7 +287,7 @@ __global__ void delta_kernel(const T* __restrict__ dO, const T* __restrict__ Out
 }
 
 template <typename T>
-__global__ void dsoftmax_kernel(const T* __restrict__ P, const T* __restrict__ dP,
+__global__ void dsoftmax_kernel(const T* __restrict__ P, const float* __restrict__ dP,
                                 const float* __restrict__ delta, T* __restrict__ dS,
                                 int64_t rows, int64_t cols, int64_t ld, float scale) {
   const int64_t r = blockIdx.y * (int64_t)gridDim.z + blockIdx.z;
@@ -295,7 +295,7 @@ __global__ void dsoftmax_kernel(const T* __restrict__ P, const T* __restrict__ d
   const float dl = delta[r];
   for (int64_t c = blockIdx.x * 256 + threadIdx.x; c < cols; c += (int64_t)gridDim.x * 256) {
     const int64_t i = r * ld + c;
-    dS[i] = from_f32<T>(to_f32(P[i]) * (to_f32(dP[i]) - dl) * scale);
+    dS[i] = from_f32<T>(to_f32(P[i]) * (dP[i] - dl) * scale);
   }
 }
 
@@ -341,7 +341,7 @@ extern "C" int comet_attn_probs(int dtype_s, const void* s, const float* lse, vo
   if (dtype_s == COMET_F32)
     hipLaunchKernelGGL((probs_kernel<float>), g, dim3(256), 0, st, (const float*)s, lse, (float*)p, rows, cols, ld_s, ld_p, scale);
   else
-    hipLaunchKernelGGL((probs_kernel<__bf16>), g, dim3(256), 0, st, (const __bf16*)s, lse, (__bf16*)p, rows, cols, ld_s, ld_p, scale);
+    hipLaunchKernelGGL((probs_kernel<__bf16>), g, dim3(256), 0, st, (const float*)s, lse, (__bf16*)p, rows, cols, ld_s, ld_p, scale);
   COMET_CHECK_LAUNCH("comet_attn_probs");
   return COMET_OK;
 }
@@ -373,7 +373,7 @@ extern "C" int comet_attn_dsoftmax(int dtype_p, const void* p, const void* dp, c
   if (dtype_p == COMET_F32)
     hipLaunchKernelGGL((dsoftmax_kernel<float>), g, dim3(256), 0, st, (const float*)p, (const float*)dp, delta, (float*)ds, rows, cols, ld, scale);
   else
-    hipLaunchKernelGGL((dsoftmax_kernel<__bf16>), g, dim3(256), 0, st, (const __bf16*)p, (const __bf16*)dp, delta, (__bf16*)ds, rows, cols, ld, scale);
+    hipLaunchKernelGGL((dsoftmax_kernel<__bf16>), g, dim3(256), 0, st, (const __bf16*)p, (const float*)dp, delta, (__bf16*)ds, rows, cols, ld, scale);
   COMET_CHECK_LAUNCH("comet_attn_dsoftmax");
   return COMET_OK;
 }

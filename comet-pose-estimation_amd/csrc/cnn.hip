@@ -16,10 +16,11 @@ __global__ void im2col_nhwc_kernel(const TI* __restrict__ x, TO* __restrict__ co
                                    int64_t h, int64_t w, int64_t c, int kh, int kw, int stride,
                                    int pad, int64_t oh, int64_t ow, int64_t ldc) {
   const int64_t kk = (int64_t)kh * kw * c;
-  const int64_t total = n * oh * ow * kk;
+  const int64_t total = n * oh * ow * ldc;
   const int64_t gs = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gs) {
-    const int64_t col = i % kk, pix = i / kk;
+    const int64_t col = i % ldc, pix = i / ldc;
+    if (col >= kk) { cols[i] = from_f32<TO>(0.f); continue; }
     const int64_t ci = col % c, kx = (col / c) % kw, ky = col / (c * kw);
     const int64_t ox = pix % ow, oy = (pix / ow) % oh, ni = pix / (ow * oh);
     const int64_t iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
@@ -80,7 +81,8 @@ extern "C" int comet_im2col_nhwc(int dtype_in, int dtype_out, const void* x, voi
                                  int pad, int64_t oh, int64_t ow, int64_t ldc, void* stream) {
   COMET_CHECK_ARG(x && cols && n > 0 && c > 0 && kh > 0 && kw > 0 && stride > 0, "comet_im2col_nhwc: bad args");
   hipStream_t s = as_stream(stream);
-  const unsigned g = g1d(n * oh * ow * kh * kw * c);
+  COMET_CHECK_ARG(ldc >= (int64_t)kh * kw * c, "comet_im2col_nhwc: ldc < kh*kw*c");
+  const unsigned g = g1d(n * oh * ow * ldc);
 #define IC(TI, TO) hipLaunchKernelGGL((im2col_nhwc_kernel<TI, TO>), dim3(g), dim3(256), 0, s, (const TI*)x, (TO*)cols, n, h, w, c, kh, kw, stride, pad, oh, ow, ldc)
   if (dtype_in == COMET_F32 && dtype_out == COMET_F32) IC(float, float);
   else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) IC(float, __bf16);

@@ -18,11 +18,11 @@ template <typename TX, typename TY>
 __global__ void __launch_bounds__(256)
 ln_fwd_kernel(const TX* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
               TY* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-              int64_t rows, int cols, float eps) {
+              int64_t rows, int cols, int64_t ldx, int64_t ldy, float eps, int relu) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const TX* xr = x + row * cols;
+  const TX* xr = x + row * ldx;
   float v[LN_MAXV];
   float s = 0.f;
 #pragma unroll
@@ -41,7 +41,7 @@ ln_fwd_kernel(const TX* __restrict__ x, const float* __restrict__ w, const float
   }
   const float var = wave_sum(q) / cols;
   const float rstd = rsqrtf(var + eps);
-  TY* yr = y + row * cols;
+  TY* yr = y + row * ldy;
 #pragma unroll
   for (int i = 0; i < LN_MAXV; ++i) {
     const int c = lane + i * 64;
@@ -49,6 +49,7 @@ ln_fwd_kernel(const TX* __restrict__ x, const float* __restrict__ w, const float
       float o = (v[i] - mean) * rstd;
       if (w) o = o * w[c];
       if (b) o = o + b[c];
+      if (relu) o = o > 0.f ? o : 0.f;
       yr[c] = from_f32<TY>(o);
     }
   }
@@ -129,7 +130,7 @@ ln_bwd_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const float* 
 template <typename T>
 __global__ void __launch_bounds__(256)
 instnorm_nhwc_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
-                     int64_t hw, int c, float eps, int relu) {
+                     int64_t hw, int c, float eps, int relu, int relu_inner) {
   __shared__ float red_s[4][64], red_q[4][64];
   const int64_t n = blockIdx.x;
   const int c0 = blockIdx.y * 64;
@@ -160,6 +161,7 @@ instnorm_nhwc_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __re
   const T* rb = res ? res + n * hw * c : nullptr;
   for (int64_t p = part; p < hw; p += 4) {
     float o = (to_f32(xb[p * c + ch]) - mean) * rstd;
+    if (relu_inner) o = o > 0.f ? o : 0.f;
     if (rb) o += to_f32(rb[p * c + ch]);
     if (relu) o = o > 0.f ? o : 0.f;
     yb[p * c + ch] = from_f32<T>(o);
@@ -173,7 +175,8 @@ using namespace comet;
 
 extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, const float* weight,
                                    const float* bias, void* y, float* mean, float* rstd,
-                                   int64_t rows, int64_t cols, float eps, void* stream) {
+                                   int64_t rows, int64_t cols, int64_t ldx, int64_t ldy, float eps,
+                                   int relu, void* stream) {
   COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_fwd: cols must be in [1,1024]");
   COMET_CHECK_ARG(x && y, "comet_layernorm_fwd: null pointer");
   if (rows == 0) return COMET_OK;
@@ -181,7 +184,7 @@ extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, cons
   hipStream_t s = as_stream(stream);
 #define LNF(TX, TY)                                                                        \
   hipLaunchKernelGGL((ln_fwd_kernel<TX, TY>), grid, dim3(256), 0, s, (const TX*)x, weight, \
-                     bias, (TY*)y, mean, rstd, rows, (int)cols, eps)
+                     bias, (TY*)y, mean, rstd, rows, (int)cols, ldx, ldy, eps, relu)
   if (dtype_x == COMET_F32 && dtype_y == COMET_F32) LNF(float, float);
   else if (dtype_x == COMET_F32 && dtype_y == COMET_BF16) LNF(float, __bf16);
   else if (dtype_x == COMET_BF16 && dtype_y == COMET_F32) LNF(__bf16, float);
@@ -217,17 +220,16 @@ extern "C" int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, con
 extern "C" int comet_instnorm_nhwc(int dtype, const void* x, const void* res, void* y, int64_t n,
                                    int64_t hw, int64_t c, float eps, int relu, int res_norm_relu,
                                    void* stream) {
-  (void)res_norm_relu;
   COMET_CHECK_ARG(x && y && n > 0 && hw > 0 && c > 0, "comet_instnorm_nhwc: bad args");
   COMET_CHECK_ARG(cdiv(c, 64) <= 65535, "comet_instnorm_nhwc: c too large");
   dim3 grid((unsigned)n, (unsigned)cdiv(c, 64));
   hipStream_t s = as_stream(stream);
   if (dtype == COMET_F32)
     hipLaunchKernelGGL((instnorm_nhwc_kernel<float>), grid, dim3(256), 0, s, (const float*)x,
-                       (const float*)res, (float*)y, hw, (int)c, eps, relu);
+                       (const float*)res, (float*)y, hw, (int)c, eps, relu, res_norm_relu);
   else if (dtype == COMET_BF16)
     hipLaunchKernelGGL((instnorm_nhwc_kernel<__bf16>), grid, dim3(256), 0, s, (const __bf16*)x,
-                       (const __bf16*)res, (__bf16*)y, hw, (int)c, eps, relu);
+                       (const __bf16*)res, (__bf16*)y, hw, (int)c, eps, relu, res_norm_relu);
   else { set_error("comet_instnorm_nhwc: bad dtype"); return COMET_EINVAL; }
   COMET_CHECK_LAUNCH("comet_instnorm_nhwc");
   return COMET_OK;

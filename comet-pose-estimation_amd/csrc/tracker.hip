@@ -1,0 +1,486 @@
+// Point-tracker kernels (coarse CoTracker-style predictor and fine refinement) + DINOv2 input
+// preparation. All feature maps are channels-last (NHWC).
+//
+// Reference sites: base_track_predictor.py:95-284 (iteration: corr sample, flow embedding,
+// transformer input, feature / coordinate update), blocks.py:351-429 (CorrBlock: avg-pool
+// pyramid, corr = f·fmap/sqrt(C), 9x9 bilinear window, zeros padding), utils.py:835-974
+// (get_2d_embedding, bilinear_sampler, sample_features4d), refine_track.py:26-278 (patch
+// extraction, compute_score_fn), E2Epose2.py:232-236 (score inversion),
+// camera_predictor10.py:622-634 (resize to 336, ImageNet normalisation) + DINOv2 patch_embed.
+#include "common.hpp"
+
+namespace comet {
+namespace {
+
+inline unsigned g1d(int64_t n) {
+  int64_t g = cdiv(n, 256);
+  return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
+}
+#define GRID_STRIDE(i, n) \
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+// torch grid_sample source index for align_corners=True after bilinear_sampler's
+// normalisation: g = x * 2/max(size-1,1) - 1 ; ix = ((g + 1) / 2) * (size - 1)
+__device__ __forceinline__ float src_index(float x, int size, bool border) {
+  const float g = x * (2.f / (float)(size - 1 > 1 ? size - 1 : 1)) - 1.f;
+  float ix = ((g + 1.f) / 2.f) * (float)(size - 1);
+  if (border) ix = fminf(fmaxf(ix, 0.f), (float)(size - 1));
+  return ix;
+}
+
+// sample_features4d: out[b, r, c] = bilinear(fmap[b], coords[b, r]) ; one wave per (b, r)
+template <typename T>
+__global__ void sample_kernel(const T* __restrict__ fmap, int64_t bstride, int H, int W, int C,
+                              const float* __restrict__ coords, int64_t cstride_b, int64_t cstride_r,
+                              float* __restrict__ out, int64_t ostride_b, int64_t ostride_r, int64_t B,
+                              int64_t R, int border) {
+  const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wv >= B * R) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = wv / R, r = wv % R;
+  const float* cp = coords + b * cstride_b + r * cstride_r;
+  const float ix = src_index(cp[0], W, border), iy = src_index(cp[1], H, border);
+  const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+  const int x1 = x0 + 1, y1 = y0 + 1;
+  const float wnw = ((float)x1 - ix) * ((float)y1 - iy), wne = (ix - (float)x0) * ((float)y1 - iy);
+  const float wsw = ((float)x1 - ix) * (iy - (float)y0), wse = (ix - (float)x0) * (iy - (float)y0);
+  const T* base = fmap + b * bstride;
+  auto ok = [&](int x, int y) { return x >= 0 && x < W && y >= 0 && y < H; };
+  for (int c = lane; c < C; c += 64) {
+    float v = 0.f;
+    if (ok(x0, y0)) v += to_f32(base[((int64_t)y0 * W + x0) * C + c]) * wnw;
+    if (ok(x1, y0)) v += to_f32(base[((int64_t)y0 * W + x1) * C + c]) * wne;
+    if (ok(x0, y1)) v += to_f32(base[((int64_t)y1 * W + x0) * C + c]) * wsw;
+    if (ok(x1, y1)) v += to_f32(base[((int64_t)y1 * W + x1) * C + c]) * wse;
+    out[b * ostride_b + r * ostride_r + c] = v;
+  }
+}
+
+// CorrBlock.corr + CorrBlock.sample fused: for track (b, n, s) and level l, window (i, j)
+// samples the correlation map f·fmap_l/sqrt(C) bilinearly (zeros padding) at
+// (x/2^l + i - r, y/2^l + j - r) (the reference's meshgrid(dy, dx) puts the first window index on
+// x). Correlation is linear, so the 4 corner dot products are formed on a (2r+4)^2 pixel grid
+// around the window and shared by all (2r+1)^2 samples. One workgroup (256 threads) per track.
+struct PyrTab {
+  const void* p[8];
+  int h[8];
+  int w[8];
+};
+
+template <typename TF, typename TT, int C>
+__global__ void __launch_bounds__(256)
+corr_kernel(PyrTab tab, int levels, int radius, const TT* __restrict__ feats, const float* __restrict__ coords,
+            float* __restrict__ out, int64_t ldo, int64_t col0, int64_t N, int S, float inv_sqrt_c) {
+  constexpr int G = 16;  // max grid side (2r+4 <= 16 -> r <= 6)
+  __shared__ float f[C];
+  __shared__ float dots[G * G];
+  const int64_t t = blockIdx.x;  // (b*N + n)*S + s
+  const int s = (int)(t % S);
+  const int64_t bn = t / S;
+  const int64_t b = bn / N;
+  for (int c = threadIdx.x; c < C; c += 256) f[c] = to_f32(feats[t * C + c]);
+  const float cx = coords[t * 2], cy = coords[t * 2 + 1];
+  const int win = 2 * radius + 1, gs = 2 * radius + 4;
+  float* orow = out + t * ldo + col0;
+  for (int l = 0; l < levels; ++l) {
+    const int H = tab.h[l], W = tab.w[l];
+    const TF* fm = reinterpret_cast<const TF*>(tab.p[l]) + (b * S + s) * (int64_t)H * W * C;
+    const float scl = 1.f / (float)(1 << l);
+    const float xl = cx * scl, yl = cy * scl;
+    const int gx0 = (int)floorf(xl) - radius - 1, gy0 = (int)floorf(yl) - radius - 1;
+    __syncthreads();
+    // dot products on the pixel grid (one wave per pixel group, lanes over channels)
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int p = wid; p < gs * gs; p += 4) {
+      const int px = gx0 + p % gs, py = gy0 + p / gs;
+      float acc = 0.f;
+      if (px >= 0 && px < W && py >= 0 && py < H) {
+        const TF* pix = fm + ((int64_t)py * W + px) * C;
+        for (int c = lane; c < C; c += 64) acc += f[c] * to_f32(pix[c]);
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) dots[(p / gs) * G + (p % gs)] = acc * inv_sqrt_c;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < win * win; k += 256) {
+      const int i = k / win, j = k % win;
+      const float ix = src_index(xl + (float)(i - radius), W, false);
+      const float iy = src_index(yl + (float)(j - radius), H, false);
+      const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+      const float wnw = ((float)(x0 + 1) - ix) * ((float)(y0 + 1) - iy), wne = (ix - (float)x0) * ((float)(y0 + 1) - iy);
+      const float wsw = ((float)(x0 + 1) - ix) * (iy - (float)y0), wse = (ix - (float)x0) * (iy - (float)y0);
+      auto D = [&](int x, int y) -> float {
+        const int gx = x - gx0, gy = y - gy0;
+        return (gx >= 0 && gx < gs && gy >= 0 && gy < gs) ? dots[gy * G + gx] : 0.f;
+      };
+      orow[l * win * win + k] = D(x0, y0) * wnw + D(x0 + 1, y0) * wne + D(x0, y0 + 1) * wsw + D(x0 + 1, y0 + 1) * wse;
+    }
+  }
+}
+
+// Transformer input of one iteration, [B*N*S, tdim] rows t = (b*N + n)*S + s (compute dtype):
+// [ flows_emb(2*E) | flows(2) | corr (already written, f32 scratch) | track feats | 0 pad ] + pos
+// where flows = coords[t] - coords[(b,n,0)], emb = get_2d_embedding(flows, E) (sin/cos
+// interleaved per axis, freqs 2k*1000/E), pos = sampled 2-D sincos row of (b, n).
+template <typename TO>
+__global__ void tokens_kernel(const float* __restrict__ coords, const float* __restrict__ feats, int latent,
+                              const float* __restrict__ corr, int64_t ldcorr, int corrdim,
+                              const float* __restrict__ pos, int tdim, TO* __restrict__ x, int64_t rows,
+                              int S) {
+  const int E = latent / 2;
+  GRID_STRIDE(i, rows * tdim) {
+    const int64_t t = i / tdim;
+    const int c = (int)(i % tdim);
+    const int64_t t0 = t - (t % S);
+    float v;
+    if (c < 2 * E + 2) {
+      const float fx = coords[t * 2] - coords[t0 * 2], fy = coords[t * 2 + 1] - coords[t0 * 2 + 1];
+      if (c >= 2 * E) {
+        v = c == 2 * E ? fx : fy;
+      } else {
+        const float a = c < E ? fx : fy;
+        const int cc = c < E ? c : c - E;
+        const float div = (float)(cc & ~1) * (1000.0f / (float)E);
+        v = (cc & 1) ? cosf(a * div) : sinf(a * div);
+      }
+    } else if (c < 2 * E + 2 + corrdim) {
+      v = corr[t * ldcorr + (c - 2 * E - 2)];
+    } else if (c < 2 * E + 2 + corrdim + latent) {
+      v = feats[t * latent + (c - 2 * E - 2 - corrdim)];
+    } else {
+      v = 0.f;
+    }
+    x[i] = from_f32<TO>(v + pos[(t / S) * tdim + c]);
+  }
+}
+
+// coords[t] += delta[t, 0:2] for s > 0 (frame 0 pinned, base_track_predictor.py:247-254);
+// preds[it][b, s, n] = coords * scale (layout [B, S, N, 2]).
+template <typename TD>
+__global__ void coords_update_kernel(float* __restrict__ coords, const TD* __restrict__ delta, int64_t ldd,
+                                     float* __restrict__ preds, float scale, int64_t B, int64_t N, int S) {
+  GRID_STRIDE(t, B * N * S) {
+    const int s = (int)(t % S);
+    const int64_t bn = t / S, b = bn / N, n = bn % N;
+    float x = coords[t * 2], y = coords[t * 2 + 1];
+    if (s > 0) {
+      x += to_f32(delta[t * ldd]);
+      y += to_f32(delta[t * ldd + 1]);
+      coords[t * 2] = x;
+      coords[t * 2 + 1] = y;
+    }
+    if (preds) {
+      const int64_t o = ((b * S + s) * N + n) * 2;
+      preds[o] = x * scale;
+      preds[o + 1] = y * scale;
+    }
+  }
+}
+
+// avg_pool2d(2, stride 2) on NHWC
+template <typename T>
+__global__ void avgpool2_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t n, int H, int W, int C) {
+  const int OH = H / 2, OW = W / 2;
+  GRID_STRIDE(i, n * OH * OW * C) {
+    const int c = (int)(i % C);
+    const int64_t p = i / C;
+    const int ox = (int)(p % OW), oy = (int)((p / OW) % OH);
+    const int64_t b = p / ((int64_t)OW * OH);
+    const T* base = x + ((b * H + 2 * oy) * W + 2 * ox) * C + c;
+    const float s = to_f32(base[0]) + to_f32(base[C]) + to_f32(base[(int64_t)W * C]) + to_f32(base[(int64_t)W * C + C]);
+    y[i] = from_f32<T>(s * 0.25f);
+  }
+}
+
+// refine_track.py:74-131: integer patch origins, 31x31 RGB patches (NHWC) and the fine query points.
+// images [B, S, 3, H, W] f32; coarse [B, S, N, 2]; patches [B*N*S, P, P, 3] in (b, n, s) order
+// (the rearrange '(b s n) -> (b n) s' of refine_track.py:123 folded into the gather);
+// topleft [B, S, N, 2] (int, unclamped), query [B*N, 2] = frac(coarse[:, 0]) + pradius.
+template <typename TO>
+__global__ void patch_gather_kernel(const float* __restrict__ images, const float* __restrict__ coarse,
+                                    TO* __restrict__ patches, int* __restrict__ topleft, float* __restrict__ query,
+                                    int64_t B, int S, int64_t N, int H, int W, int pradius) {
+  const int P = 2 * pradius + 1;
+  GRID_STRIDE(i, B * S * N * P * P * 3) {
+    const int ci = (int)(i % 3);
+    const int64_t q = i / 3;
+    const int px = (int)(q % P), py = (int)((q / P) % P);
+    const int64_t tp = q / ((int64_t)P * P);  // patch order (b*N + n)*S + s (fine-tracker layout)
+    const int sp = (int)(tp % S);
+    const int64_t np_ = (tp / S) % N, bp = tp / ((int64_t)S * N);
+    const int64_t t = (bp * S + sp) * N + np_;  // coarse / topleft order (b*S + s)*N + n
+    const float cx = coarse[t * 2], cy = coarse[t * 2 + 1];
+    const int ix = (int)floorf(cx), iy = (int)floorf(cy);
+    const int tlx = ix - pradius, tly = iy - pradius;
+    const int lim = H - P;  // the reference clamps both axes with H (assumes H == W)
+    const int x0 = tlx < 0 ? 0 : (tlx > lim ? lim : tlx);
+    const int y0 = tly < 0 ? 0 : (tly > lim ? lim : tly);
+    const int64_t bs = t / N;
+    patches[i] = from_f32<TO>(images[((bs * 3 + ci) * H + (y0 + py)) * (int64_t)W + (x0 + px)]);
+    if (px == 0 && py == 0 && ci == 0) {
+      topleft[t * 2] = tlx;
+      topleft[t * 2 + 1] = tly;
+      const int s = (int)(bs % S);
+      if (s == 0) {
+        const int64_t b = bs / S, n = t % N;
+        query[(b * N + n) * 2] = (cx - (float)ix) + (float)pradius;
+        query[(b * N + n) * 2 + 1] = (cy - (float)iy) + (float)pradius;
+      }
+    }
+  }
+}
+
+// refined[b, s, n] = fine_last[(b*N+n), s] + topleft[b, s, n]; frame 0 = coarse query point.
+__global__ void refine_combine_kernel(const float* __restrict__ fine, const int* __restrict__ topleft,
+                                      const float* __restrict__ coarse, float* __restrict__ refined,
+                                      int64_t B, int S, int64_t N) {
+  GRID_STRIDE(t, B * S * N) {
+    const int64_t n = t % N, bs = t / N, s = bs % S, b = bs / S;
+    if (s == 0) {
+      refined[t * 2] = coarse[(b * S * N + n) * 2];
+      refined[t * 2 + 1] = coarse[(b * S * N + n) * 2 + 1];
+    } else {
+      const int64_t f = ((b * N + n) * S + s) * 2;
+      refined[t * 2] = fine[f] + (float)topleft[t * 2];
+      refined[t * 2 + 1] = fine[f + 1] + (float)topleft[t * 2 + 1];
+    }
+  }
+}
+
+// compute_score_fn (refine_track.py:174-278) + score inversion (E2Epose2.py:232-236), one thread
+// per (b, n). Reproduces the reference's indexing: the feature map of every window is patch
+// (s = 0, n = 0) of the sequence (batch_indices = arange(B) indexes the flat (b s n) axis), and
+// the window origin for output (b, s, n) is read from the fine track at flat position
+// m = (b*S + s)*N + n of its (b n, s) layout. Window row = clamp(floor(y)-r), col = clamp(floor(x)-r).
+template <typename TF>
+__global__ void score_kernel(const float* __restrict__ qfeat, const TF* __restrict__ pfeat,
+                             const float* __restrict__ fine, float* __restrict__ score,
+                             float* __restrict__ inv_score, int64_t B, int S, int64_t N, int P, int C,
+                             int sradius) {
+  const int ss = 2 * sradius + 1;
+  const float lin_step = 2.f / (float)(ss - 1);
+  GRID_STRIDE(t, B * N) {
+    const int64_t b = t / N, n = t % N;
+    const float* q = qfeat + t * C;
+    // feature map f = patch (b, s=0, n=0): row (b*N + 0) of [B*N, S, P, P, C], frame 0
+    const TF* fm = pfeat + (b * N * S) * (int64_t)P * P * C;
+    float inv_max = 0.f;
+    for (int s = 0; s < S; ++s) {
+      float sc = 1.f;
+      if (s > 0) {
+        const int64_t m = (b * S + s) * N + n;  // flat (b s n) position
+        const int64_t bn2 = m / S;              // read in (b n, s) order
+        const int s2 = (int)(m % S);
+        const float fx = fine[(bn2 * S + s2) * 2], fy = fine[(bn2 * S + s2) * 2 + 1];
+        int tx = (int)floorf(fx) - sradius, ty = (int)floorf(fy) - sradius;
+        const int lim = P - ss;
+        tx = tx < 0 ? 0 : (tx > lim ? lim : tx);
+        ty = ty < 0 ? 0 : (ty > lim ? lim : ty);
+        float sim[25];
+        float mx = -INFINITY;
+        for (int a = 0; a < ss; ++a)
+          for (int c2 = 0; c2 < ss; ++c2) {
+            const TF* pix = fm + ((int64_t)(ty + a) * P + (tx + c2)) * C;
+            float d = 0.f;
+            for (int c = 0; c < C; ++c) d += q[c] * to_f32(pix[c]);
+            d *= 1.f / sqrtf((float)C);
+            sim[a * ss + c2] = d;
+            mx = fmaxf(mx, d);
+          }
+        float den = 0.f;
+        for (int k = 0; k < ss * ss; ++k) { sim[k] = expf(sim[k] - mx); den += sim[k]; }
+        float ex = 0.f, ey = 0.f, ex2 = 0.f, ey2 = 0.f;
+        for (int a = 0; a < ss; ++a)
+          for (int c2 = 0; c2 < ss; ++c2) {
+            const float p = sim[a * ss + c2] / den;
+            const float gx = -1.f + lin_step * (float)c2, gy = -1.f + lin_step * (float)a;
+            ex += p * gx; ey += p * gy; ex2 += p * gx * gx; ey2 += p * gy * gy;
+          }
+        sc = sqrtf(fmaxf(ex2 - ex * ex, 1e-10f)) + sqrtf(fmaxf(ey2 - ey * ey, 1e-10f));
+      }
+      score[(b * S + s) * N + n] = sc;
+      const float iv = 1.f / (sc + 1e-6f);
+      inv_score[(b * S + s) * N + n] = iv;
+      inv_max = fmaxf(inv_max, iv);
+    }
+    for (int s = 0; s < S; ++s) inv_score[(b * S + s) * N + n] /= inv_max;
+  }
+}
+
+// DINOv2 input: x [BS, 3, H, W] f32 -> bilinear(align_corners) to R x R -> (x - mean)/std ->
+// patch rows cols[(f*g + py)*g + px][ci*p*p + ky*p + kx] (conv weight flatten order), K padded.
+template <typename TO>
+__global__ void dino_prep_kernel(const float* __restrict__ x, TO* __restrict__ cols, int64_t BS, int H, int W,
+                                 int R, int patch, int64_t ldc, float m0, float m1, float m2, float s0, float s1,
+                                 float s2) {
+  const int g = R / patch;
+  const int kk = 3 * patch * patch;
+  const float scy = R > 1 ? (float)(H - 1) / (float)(R - 1) : 0.f;
+  const float scx = R > 1 ? (float)(W - 1) / (float)(R - 1) : 0.f;
+  GRID_STRIDE(i, BS * g * g * ldc) {
+    const int64_t col = i % ldc, row = i / ldc;
+    if (col >= kk) { cols[i] = from_f32<TO>(0.f); continue; }
+    const int ci = (int)(col / (patch * patch)), ky = (int)((col / patch) % patch), kx = (int)(col % patch);
+    const int px = (int)(row % g), py = (int)((row / g) % g);
+    const int64_t f = row / ((int64_t)g * g);
+    const int oy = py * patch + ky, ox = px * patch + kx;
+    const float sy = scy * (float)oy, sx = scx * (float)ox;
+    int y0 = (int)sy; if (y0 > H - 1) y0 = H - 1;
+    int x0 = (int)sx; if (x0 > W - 1) x0 = W - 1;
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+    const float ly = sy - (float)y0, lx = sx - (float)x0;
+    const float* pl = x + (f * 3 + ci) * (int64_t)H * W;
+    const float v = (1.f - ly) * ((1.f - lx) * pl[(int64_t)y0 * W + x0] + lx * pl[(int64_t)y0 * W + x1]) +
+                    ly * ((1.f - lx) * pl[(int64_t)y1 * W + x0] + lx * pl[(int64_t)y1 * W + x1]);
+    const float mean = ci == 0 ? m0 : (ci == 1 ? m1 : m2);
+    const float sd = ci == 0 ? s0 : (ci == 1 ? s1 : s2);
+    cols[i] = from_f32<TO>((v - mean) / sd);
+  }
+}
+
+}  // namespace
+}  // namespace comet
+
+using namespace comet;
+
+extern "C" int comet_sample_bilinear(int dtype, const void* fmap, int64_t bstride, int H, int W, int C,
+                                     const float* coords, int64_t cstride_b, int64_t cstride_r, float* out,
+                                     int64_t ostride_b, int64_t ostride_r, int64_t B, int64_t R, int border,
+                                     void* stream) {
+  COMET_CHECK_ARG(fmap && coords && out && H > 0 && W > 0 && C > 0, "comet_sample_bilinear: bad args");
+  if (B * R == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  dim3 g((unsigned)cdiv(B * R, 4));
+  if (dtype == COMET_F32)
+    hipLaunchKernelGGL((sample_kernel<float>), g, dim3(256), 0, s, (const float*)fmap, bstride, H, W, C, coords,
+                       cstride_b, cstride_r, out, ostride_b, ostride_r, B, R, border);
+  else
+    hipLaunchKernelGGL((sample_kernel<__bf16>), g, dim3(256), 0, s, (const __bf16*)fmap, bstride, H, W, C, coords,
+                       cstride_b, cstride_r, out, ostride_b, ostride_r, B, R, border);
+  COMET_CHECK_LAUNCH("comet_sample_bilinear");
+  return COMET_OK;
+}
+
+extern "C" int comet_corr_sample(int dtype_fmap, int dtype_feat, const void* const* pyramid, const int* heights,
+                                 const int* widths, int levels, int radius, int C, const void* feats,
+                                 const float* coords, float* out, int64_t ldo, int64_t col0, int64_t B,
+                                 int64_t N, int S, void* stream) {
+  COMET_CHECK_ARG(levels >= 1 && levels <= 8 && radius >= 1 && radius <= 6, "comet_corr_sample: levels in [1,8], radius in [1,6]");
+  COMET_CHECK_ARG(C == 128 || C == 32, "comet_corr_sample: C must be 128 (coarse) or 32 (fine)");
+  COMET_CHECK_ARG(pyramid && heights && widths && feats && coords && out, "comet_corr_sample: null pointer");
+  COMET_CHECK_ARG(dtype_feat == COMET_F32, "comet_corr_sample: track features must be f32");
+  const int64_t T = B * N * S;
+  if (T == 0) return COMET_OK;
+  COMET_CHECK_ARG(T < (1ll << 31), "comet_corr_sample: too many tracks");
+  PyrTab tab{};
+  for (int l = 0; l < levels; ++l) {
+    COMET_CHECK_ARG(pyramid[l] != nullptr, "comet_corr_sample: null level");
+    tab.p[l] = pyramid[l]; tab.h[l] = heights[l]; tab.w[l] = widths[l];
+  }
+  hipStream_t s = as_stream(stream);
+  const float isc = 1.f / sqrtf((float)C);
+#define CK(TF, CC) hipLaunchKernelGGL((corr_kernel<TF, float, CC>), dim3((unsigned)T), dim3(256), 0, s, tab, levels, radius, (const float*)feats, coords, out, ldo, col0, N, S, isc)
+  if (dtype_fmap == COMET_F32) { if (C == 128) CK(float, 128); else CK(float, 32); }
+  else { if (C == 128) CK(__bf16, 128); else CK(__bf16, 32); }
+#undef CK
+  COMET_CHECK_LAUNCH("comet_corr_sample");
+  return COMET_OK;
+}
+
+extern "C" int comet_tracker_tokens(int dtype_out, const float* coords, const float* feats, int latent,
+                                    const float* corr, int64_t ldcorr, int corrdim, const float* pos, int tdim,
+                                    void* x, int64_t rows, int S, void* stream) {
+  COMET_CHECK_ARG(coords && feats && corr && pos && x && tdim >= latent * 2 + 2 + corrdim, "comet_tracker_tokens: bad args");
+  if (rows == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype_out == COMET_F32)
+    hipLaunchKernelGGL((tokens_kernel<float>), dim3(g1d(rows * tdim)), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (float*)x, rows, S);
+  else
+    hipLaunchKernelGGL((tokens_kernel<__bf16>), dim3(g1d(rows * tdim)), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (__bf16*)x, rows, S);
+  COMET_CHECK_LAUNCH("comet_tracker_tokens");
+  return COMET_OK;
+}
+
+extern "C" int comet_coords_update(int dtype_delta, float* coords, const void* delta, int64_t ldd, float* preds,
+                                   float scale, int64_t B, int64_t N, int S, void* stream) {
+  COMET_CHECK_ARG(coords && delta, "comet_coords_update: null pointer");
+  if (B * N * S == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype_delta == COMET_F32)
+    hipLaunchKernelGGL((coords_update_kernel<float>), dim3(g1d(B * N * S)), dim3(256), 0, s, coords, (const float*)delta, ldd, preds, scale, B, N, S);
+  else
+    hipLaunchKernelGGL((coords_update_kernel<__bf16>), dim3(g1d(B * N * S)), dim3(256), 0, s, coords, (const __bf16*)delta, ldd, preds, scale, B, N, S);
+  COMET_CHECK_LAUNCH("comet_coords_update");
+  return COMET_OK;
+}
+
+extern "C" int comet_avgpool2_nhwc(int dtype, const void* x, void* y, int64_t n, int H, int W, int C, void* stream) {
+  COMET_CHECK_ARG(x && y && H >= 2 && W >= 2, "comet_avgpool2_nhwc: bad args");
+  hipStream_t s = as_stream(stream);
+  const int64_t tot = n * (H / 2) * (W / 2) * C;
+  if (dtype == COMET_F32)
+    hipLaunchKernelGGL((avgpool2_kernel<float>), dim3(g1d(tot)), dim3(256), 0, s, (const float*)x, (float*)y, n, H, W, C);
+  else
+    hipLaunchKernelGGL((avgpool2_kernel<__bf16>), dim3(g1d(tot)), dim3(256), 0, s, (const __bf16*)x, (__bf16*)y, n, H, W, C);
+  COMET_CHECK_LAUNCH("comet_avgpool2_nhwc");
+  return COMET_OK;
+}
+
+extern "C" int comet_patch_gather(int dtype_out, const float* images, const float* coarse, void* patches,
+                                  int* topleft, float* query, int64_t B, int S, int64_t N, int H, int W,
+                                  int pradius, void* stream) {
+  COMET_CHECK_ARG(images && coarse && patches && topleft && query, "comet_patch_gather: null pointer");
+  COMET_CHECK_ARG(H >= 2 * pradius + 1 && W >= 2 * pradius + 1, "comet_patch_gather: image smaller than a patch");
+  const int P = 2 * pradius + 1;
+  const int64_t tot = B * S * N * P * P * 3;
+  if (tot == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype_out == COMET_F32)
+    hipLaunchKernelGGL((patch_gather_kernel<float>), dim3(g1d(tot)), dim3(256), 0, s, images, coarse, (float*)patches, topleft, query, B, S, N, H, W, pradius);
+  else
+    hipLaunchKernelGGL((patch_gather_kernel<__bf16>), dim3(g1d(tot)), dim3(256), 0, s, images, coarse, (__bf16*)patches, topleft, query, B, S, N, H, W, pradius);
+  COMET_CHECK_LAUNCH("comet_patch_gather");
+  return COMET_OK;
+}
+
+extern "C" int comet_refine_combine(const float* fine, const int* topleft, const float* coarse, float* refined,
+                                    int64_t B, int S, int64_t N, void* stream) {
+  COMET_CHECK_ARG(fine && topleft && coarse && refined, "comet_refine_combine: null pointer");
+  if (B * S * N == 0) return COMET_OK;
+  hipLaunchKernelGGL(refine_combine_kernel, dim3(g1d(B * S * N)), dim3(256), 0, as_stream(stream), fine, topleft,
+                     coarse, refined, B, S, N);
+  COMET_CHECK_LAUNCH("comet_refine_combine");
+  return COMET_OK;
+}
+
+extern "C" int comet_track_score(int dtype_feat, const float* qfeat, const void* pfeat, const float* fine,
+                                 float* score, float* inv_score, int64_t B, int S, int64_t N, int P, int C,
+                                 int sradius, void* stream) {
+  COMET_CHECK_ARG(qfeat && pfeat && fine && score && inv_score, "comet_track_score: null pointer");
+  COMET_CHECK_ARG(sradius >= 1 && sradius <= 2 && P > 2 * sradius, "comet_track_score: sradius must be 1 or 2");
+  if (B * N == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype_feat == COMET_F32)
+    hipLaunchKernelGGL((score_kernel<float>), dim3(g1d(B * N)), dim3(256), 0, s, qfeat, (const float*)pfeat, fine, score, inv_score, B, S, N, P, C, sradius);
+  else
+    hipLaunchKernelGGL((score_kernel<__bf16>), dim3(g1d(B * N)), dim3(256), 0, s, qfeat, (const __bf16*)pfeat, fine, score, inv_score, B, S, N, P, C, sradius);
+  COMET_CHECK_LAUNCH("comet_track_score");
+  return COMET_OK;
+}
+
+extern "C" int comet_dino_prep(int dtype_out, const float* images, void* cols, int64_t BS, int H, int W, int R,
+                               int patch, int64_t ldc, const float* mean3, const float* std3, void* stream) {
+  COMET_CHECK_ARG(images && cols && mean3 && std3 && R % patch == 0 && ldc >= 3 * patch * patch, "comet_dino_prep: bad args");
+  const int g = R / patch;
+  const int64_t tot = BS * g * g * ldc;
+  if (tot == 0) return COMET_OK;
+  hipStream_t s = as_stream(stream);
+  if (dtype_out == COMET_F32)
+    hipLaunchKernelGGL((dino_prep_kernel<float>), dim3(g1d(tot)), dim3(256), 0, s, images, (float*)cols, BS, H, W, R, patch, ldc,
+                       mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2]);
+  else
+    hipLaunchKernelGGL((dino_prep_kernel<__bf16>), dim3(g1d(tot)), dim3(256), 0, s, images, (__bf16*)cols, BS, H, W, R, patch, ldc,
+                       mean3[0], mean3[1], mean3[2], std3[0], std3[1], std3[2]);
+  COMET_CHECK_LAUNCH("comet_dino_prep");
+  return COMET_OK;
+}

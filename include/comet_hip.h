@@ -79,10 +79,13 @@ int comet_gemm(const comet_gemm_args* args, void* stream);
  * by base_track_predictor.py:81,238). weight/bias f32 or NULL (elementwise_affine=False,
  * modules.py:261-317). mean/rstd (f32, [rows]) are written when non-NULL (for backward).
  * Output dtype may differ from input dtype (f32 residual stream -> bf16 GEMM operand).
+ * ldx / ldy are row strides (elements); relu != 0 applies ReLU after the affine
+ * (TrajectoryEncoder LN -> ReLU, camera_predictor10.py:79-81).
  * ------------------------------------------------------------------------------------- */
 int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, const float* weight,
                         const float* bias, void* y, float* mean, float* rstd,
-                        int64_t rows, int64_t cols, float eps, void* stream);
+                        int64_t rows, int64_t cols, int64_t ldx, int64_t ldy, float eps,
+                        int relu, void* stream);
 /* dx (f32) = LN backward; dweight/dbias (f32) are ACCUMULATED (+=) when non-NULL.
  * dx_accumulate != 0 adds into dx instead of overwriting. */
 int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy,
@@ -112,11 +115,12 @@ typedef struct comet_attn_args {
 int comet_attention_fwd(const comet_attn_args* args, void* stream);
 
 /* Attention backward helpers (materialised form, head_dim-agnostic):
- * probs[r, j] = exp(s[r, j]*scale - lse[r]); rows = batch*heads*lq, ld = row stride. */
+ * probs[r, j] = exp(s[r, j]*scale - lse[r]); s is f32, probs has dtype_s (the compute dtype);
+ * rows = batch*heads*lq, ld = row stride. */
 int comet_attn_probs(int dtype_s, const void* s, const float* lse, void* p, int64_t rows,
                      int64_t cols, int64_t ld_s, int64_t ld_p, float scale, void* stream);
 /* dS[r, j] = P[r, j] * (dP[r, j] - delta[r]) * scale, delta[r] = sum_d dO[r,d]*O[r,d]
- * (computed by comet_attn_delta). */
+ * (computed by comet_attn_delta). P and dS have dtype_p, dP is f32. */
 int comet_attn_delta(int dtype, const void* dout, const void* out, float* delta, int64_t batch,
                      int64_t heads, int64_t lq, int64_t d, int64_t so_b, int64_t so_h,
                      int64_t so_l, int64_t sdo_b, int64_t sdo_h, int64_t sdo_l, void* stream);
@@ -148,12 +152,14 @@ int comet_adamw_multi(float* const* params, const float* const* grads, float* co
 /* ---------------------------------------------------------------------------------------
  * Convolution / CNN operators (channels-last NHWC activations).
  * ------------------------------------------------------------------------------------- */
-/* im2col for conv2d NHWC input [n, h, w, c] -> cols [n*oh*ow, kh*kw*c] (zero padding). */
+/* im2col for conv2d NHWC input [n, h, w, c] -> cols [n*oh*ow, ldc], column (ky*kw+kx)*c+ci,
+ * columns [kh*kw*c, ldc) zero-filled (K padded to the GEMM vector width). */
 int comet_im2col_nhwc(int dtype_in, int dtype_out, const void* x, void* cols, int64_t n,
                       int64_t h, int64_t w, int64_t c, int kh, int kw, int stride, int pad,
                       int64_t oh, int64_t ow, int64_t ldc, void* stream);
 /* InstanceNorm2d (affine=False, eps 1e-5) on NHWC, optional residual add and ReLU:
- * y = relu?( IN(x) + (res ? res : 0) ). res may be NULL. */
+ * o = IN(x); if res_norm_relu: o = relu(o); if res: o += res; if relu: o = relu(o).
+ * (ResidualBlock tail relu(x + relu(IN(conv2(.)))), modules.py:108-116). */
 int comet_instnorm_nhwc(int dtype, const void* x, const void* res, void* y, int64_t n,
                         int64_t hw, int64_t c, float eps, int relu, int res_norm_relu,
                         void* stream);
@@ -162,6 +168,96 @@ int comet_instnorm_nhwc(int dtype, const void* x, const void* res, void* y, int6
 int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, const void* x, void* y,
                           int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
                           int add, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Camera head (camera_predictor10.py:329-484) and encoders.
+ * ------------------------------------------------------------------------------------- */
+/* y = act(x) elementwise (ReLU / GELU / sigmoid of the T_P gating MLPs) */
+int comet_act_fwd(int act, int dtype_x, int dtype_y, const void* x, void* y, int64_t n, void* stream);
+/* op 0: y = a + b; 1: y = relu(a + b); 2: y = a * b (same dtype, same shape) */
+int comet_binary(int op, int dtype, const void* a, const void* b, void* y, int64_t n, void* stream);
+/* y[r, c] = x[r, c] + table[r % period, c] (positional / time embeddings, table f32) */
+int comet_add_rows(int dtype_x, int dtype_y, const void* x, const float* table, void* y, int64_t rows,
+                   int64_t cols, int64_t period, int64_t ldx, int64_t ldy, void* stream);
+/* T_P confidence gating traj * w (camera_predictor10.py:332-333): y[r, :] = x[r, :] * w[r];
+ * backward dx = dy * w, dw[r] = <dy[r], x[r]> (dx / dw may be NULL) */
+int comet_rowscale_fwd(int dtype, const void* x, const float* w, void* y, int64_t rows, int64_t cols,
+                       void* stream);
+int comet_rowscale_bwd(int dtype, const void* x, const float* w, const float* dy, float* dx, float* dw,
+                       int64_t rows, int64_t cols, void* stream);
+/* 1-D sin/cos table (utils.py:807-832, double math, f32 out): out[m*ld + col0 + d] */
+int comet_sincos_table(const float* pos, float* out, int64_t m, int dim, int64_t ld, int64_t col0,
+                       void* stream);
+/* HarmonicEmbedding (minipytorch3d/harmonic_embedding.py:127-158): x [rows, dim], optional
+ * diag_cov [rows, dim], freqs [n] -> y [rows, dim*(2n + append)]; backward gives dx, dcov. */
+int comet_harmonic_fwd(const float* x, const float* diag_cov, const float* freqs, float* y, int64_t rows,
+                       int dim, int n_freqs, int append_input, void* stream);
+int comet_harmonic_bwd(const float* x, const float* diag_cov, const float* freqs, const float* dy,
+                       float* dx, float* dcov, int64_t rows, int dim, int n_freqs, int append_input,
+                       void* stream);
+/* camera_to_pose_encoding2 per sequence (utils.py:631-688): R [B*S,4], T_uvz [B*S,3],
+ * focal [B*S,2] -> enc [B*S,8]; ratio as in the reference (float64). */
+int comet_pose_encode(const float* R, const float* T_uvz, const float* focal, double ratio, float* enc,
+                      int64_t B, int S, void* stream);
+/* pose_encoding_to_camera2 per sequence (utils.py:312-403): enc [B*S,7] -> R [B*S,4] (f32),
+ * T [B*S,3] (f64, as the reference's float64 promotion), intrinsics fx, fy, cx, cy. */
+int comet_pose_decode(const float* enc, const float* R_gt, const float* T_uvz_gt, double ratio, double fx,
+                      double fy, double cx, double cy, float* R_out, double* T_out, int64_t B, int S,
+                      void* stream);
+/* GAPR head + pose loss (camera_predictor10.py:385-460): F.normalize(rot, eps 1e-8), loss =
+ * w_trans*100*MSE(uvd[1:]) + w_rot*100*MSE(q[1:]) (mean over sequences), frame-0 reset.
+ * gt_enc may be NULL (no loss). qn [B*S,4] is kept for the backward. */
+int comet_gapr_fwd(const float* rot, int64_t ld_rot, const float* uv, int64_t ld_uv, const float* d,
+                   int64_t ld_d, const float* gt_enc, float* qn, float* enc, float* losses, int B, int S,
+                   float w_trans, float w_rot, void* stream);
+/* dlosses[3] = upstream grads of (loss, loss_trans, loss_rot) (device) -> drot [B*S,4],
+ * duv [B*S,2], dd [B*S,1] */
+int comet_gapr_bwd(const float* rot, int64_t ld_rot, const float* uv, int64_t ld_uv, const float* d,
+                   int64_t ld_d, const float* gt_enc, const float* qn, const float* dlosses, float* drot,
+                   float* duv, float* dd, int B, int S, float w_trans, float w_rot, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Point tracker (base_track_predictor.py, blocks.py:351-429, refine_track.py) and DINOv2 input.
+ * Feature maps are NHWC [n, H, W, C]; track state is [B, N, S, .] (row t = (b*N + n)*S + s).
+ * ------------------------------------------------------------------------------------- */
+/* sample_features4d / bilinear_sampler (utils.py:874-974): align_corners=True pixel coords,
+ * border (1) or zeros (0) padding; out f32 [B, R, C] (element strides given). */
+int comet_sample_bilinear(int dtype, const void* fmap, int64_t bstride, int H, int W, int C,
+                          const float* coords, int64_t cstride_b, int64_t cstride_r, float* out,
+                          int64_t ostride_b, int64_t ostride_r, int64_t B, int64_t R, int border,
+                          void* stream);
+/* CorrBlock.corr + .sample fused (blocks.py:376-429): pyramid[l] NHWC [B*S, H_l, W_l, C],
+ * feats f32 [B*N*S, C], coords f32 [B*N*S, 2] (level-0 units) -> out[t*ldo + col0 + l*(2r+1)^2 + k] */
+int comet_corr_sample(int dtype_fmap, int dtype_feat, const void* const* pyramid, const int* heights,
+                      const int* widths, int levels, int radius, int C, const void* feats,
+                      const float* coords, float* out, int64_t ldo, int64_t col0, int64_t B, int64_t N,
+                      int S, void* stream);
+/* transformer input (base_track_predictor.py:170-221): [flow emb | flows | corr | feats | pad] + pos */
+int comet_tracker_tokens(int dtype_out, const float* coords, const float* feats, int latent,
+                         const float* corr, int64_t ldcorr, int corrdim, const float* pos, int tdim,
+                         void* x, int64_t rows, int S, void* stream);
+/* coords += delta[:, :2] (frame 0 pinned); preds [B, S, N, 2] = coords * scale (may be NULL) */
+int comet_coords_update(int dtype_delta, float* coords, const void* delta, int64_t ldd, float* preds,
+                        float scale, int64_t B, int64_t N, int S, void* stream);
+/* F.avg_pool2d(2, 2) on NHWC (CorrBlock pyramid, blocks.py:369-374) */
+int comet_avgpool2_nhwc(int dtype, const void* x, void* y, int64_t n, int H, int W, int C, void* stream);
+/* refine_track.py:74-131: patches NHWC [B*N*S, P, P, 3] in (b, n, s) order, topleft [B,S,N,2]
+ * (int, unclamped), query [B*N,2] = frac(coarse[:, 0]) + pradius */
+int comet_patch_gather(int dtype_out, const float* images, const float* coarse, void* patches,
+                       int* topleft, float* query, int64_t B, int S, int64_t N, int H, int W,
+                       int pradius, void* stream);
+/* refined[b,s,n] = fine[(b*N+n), s] + topleft[b,s,n]; frame 0 = coarse query (refine_track.py:143-153) */
+int comet_refine_combine(const float* fine, const int* topleft, const float* coarse, float* refined,
+                         int64_t B, int S, int64_t N, void* stream);
+/* compute_score_fn + score inversion (refine_track.py:174-278, E2Epose2.py:232-236):
+ * qfeat [B*N, C], pfeat NHWC [B*N, S, P, P, C], fine [B*N, S, 2] -> score, inv_score [B, S, N] */
+int comet_track_score(int dtype_feat, const float* qfeat, const void* pfeat, const float* fine,
+                      float* score, float* inv_score, int64_t B, int S, int64_t N, int P, int C,
+                      int sradius, void* stream);
+/* camera_predictor10.py:624-634 + DINOv2 patch_embed im2col: images [BS,3,H,W] -> resize to
+ * R (align_corners) -> (x-mean)/std -> cols [BS*(R/p)^2, ldc], column ci*p*p + ky*p + kx */
+int comet_dino_prep(int dtype_out, const float* images, void* cols, int64_t BS, int H, int W, int R,
+                    int patch, int64_t ldc, const float* mean3, const float* std3, void* stream);
 
 #ifdef __cplusplus
 }
