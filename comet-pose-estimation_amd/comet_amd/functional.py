@@ -10,23 +10,28 @@ Precision policy (mirrors accelerate mixed_precision="bf16" autocast, abl_ours.y
     gradients w.r.t. parameters: f32.
 """
 import contextlib
-import threading
 
 import torch
 
 from . import _lib as L
 from . import ops
 
-_state = threading.local()
+
+class _State:
+    # process-wide (NOT thread-local): autograd runs backward on its own device thread
+    dtype = torch.bfloat16
+
+
+_state = _State()
 
 
 def compute_dtype():
-    return getattr(_state, "dtype", torch.bfloat16)
+    return _state.dtype
 
 
 @contextlib.contextmanager
 def precision(dtype):
-    old = compute_dtype()
+    old = _state.dtype
     _state.dtype = dtype
     try:
         yield
@@ -40,10 +45,10 @@ def precision(dtype):
 _wcache = {}
 
 
-def wcast(p):
+def wcast(p, dt=None):
     """p (an f32 parameter or a view of one) in the compute dtype; cached by storage address
     and shape, so the frozen tracker / DINOv2 weights are cast once."""
-    dt = compute_dtype()
+    dt = dt or compute_dtype()
     if p.dtype == dt:
         return p
     key = (p.data_ptr(), tuple(p.shape), tuple(p.stride()), dt)
@@ -124,7 +129,8 @@ def _linear_bwd(x2, wc, dpre, need_dx, need_dw, need_db, dx_dtype):
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, resid, act, beta, out_dtype):
-        wc = wcast(w)
+        ctx.cdt = compute_dtype()
+        wc = wcast(w, ctx.cdt)
         xc = x if x.dtype == wc.dtype else ops.cast(x, wc.dtype)
         shp = x.shape
         x2 = xc.reshape(-1, shp[-1])
@@ -147,7 +153,7 @@ class _Linear(torch.autograd.Function):
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
         dpre = ops.act_bwd(ctx.act, aux, dy2, out_dtype=torch.float32) if ctx.act != L.ACT_NONE else dy2
-        wc = wcast(w)
+        wc = wcast(w, ctx.cdt)
         dx, dw, db = _linear_bwd(x2, wc, dpre, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
                                  ctx.has_b and ctx.needs_input_grad[2], torch.float32)
         if dx is not None:

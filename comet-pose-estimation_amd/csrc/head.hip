@@ -98,8 +98,8 @@ __global__ void harmonic_fwd_kernel(const float* __restrict__ x, const float* __
     } else {
       const int p = (int)(c / ((int64_t)dim * n));
       const int i = (int)((c / n) % dim), k = (int)(c % n);
-      const float e = x[r * dim + i] * freqs[k];
-      v = sinf(e + (p ? half_pi : 0.f));
+      const float e = x[r * dim + i] * freqs[k] + (p ? half_pi : 0.f);  // f32 argument, as the reference
+      v = (float)sin((double)e);  // correctly rounded: large |x*f| would lose accuracy in sinf
       if (cov) v *= expf(-0.5f * (cov[r * dim + i] * (freqs[k] * freqs[k])));
     }
     y[t] = v;
@@ -124,8 +124,8 @@ __global__ void harmonic_bwd_kernel(const float* __restrict__ x, const float* __
         const float e = xv * f + (p ? half_pi : 0.f);
         const float att = cov ? expf(-0.5f * (cov[r * dim + i] * (f * f))) : 1.f;
         const float g = dy[r * width + (int64_t)p * dim * n + (int64_t)i * n + k];
-        gx += g * cosf(e) * f * att;
-        if (cov) gc += g * sinf(e) * att * (-0.5f * f * f);
+        gx += g * (float)cos((double)e) * f * att;
+        if (cov) gc += g * (float)sin((double)e) * att * (-0.5f * f * f);
       }
     dx[t] = gx;
     if (dcov) dcov[t] = gc;
