@@ -1,0 +1,193 @@
+"""COMET train-step throughput on MI355X (BASELINE.json metric):
+sequences/s of train_e2epose2.py fwd+bwd bf16, B=8 per GPU, T=16, 512x512, N=512 tracks.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = full COMET forward (coarse + fine tracker, DINOv2, camera head; tracker/backbone
+frozen under no_grad as in the reference) + pose loss + backward through the camera head + RCCL
+gradient all-reduce (N > 1) + clip_grad_norm_(1.0) + AdamW + LR schedule. Inputs are synthetic
+and resident in HBM before timing; weights are random-init (reference initialisers).
+Rank 0 prints one JSON line. Per-GPU batch is fixed (weak scaling).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "comet-pose-estimation_amd"))
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=8, help="sequences per GPU")
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--image", type=int, default=512)
+    ap.add_argument("--tracks", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-only", action="store_true")
+    return ap.parse_args()
+
+
+def synthetic(B, T, S_img, N, device, seed):
+    g = torch.Generator(device=device).manual_seed(seed)
+    img = torch.randn(B, T, 3, S_img, S_img, device=device, generator=g)
+    kp = torch.rand(B, 1, N, 2, device=device, generator=g) * (S_img - 1)
+    tracks = kp.expand(B, T, N, 2).contiguous()
+    q = torch.randn(B * T, 4, device=device, generator=g)
+    q = q / q.norm(dim=-1, keepdim=True)
+    q = torch.where(q[:, :1] < 0, -q, q)
+    u = torch.rand(B * T, 3, device=device, generator=g)
+    uvz = torch.stack([270 + 100 * u[:, 0], 190 + 100 * u[:, 1], 5 + 10 * u[:, 2]], -1)
+    from comet_amd.models.utils import QuaternionCameras
+    cams = QuaternionCameras(R=q, T_uvz=uvz, T=torch.randn(B * T, 3, device=device, generator=g),
+                             focal_length=torch.full((B * T, 2), 268.44, device=device),
+                             ratio=torch.tensor([0.5], dtype=torch.float64), device=device)
+    return img, tracks, cams
+
+
+def cpu_baseline(T, S_img, N):
+    """The oracle (CPU fp32 restatement of the reference path) timed on this host: one
+    sequence (B=1), full train step fwd + bwd + clip + AdamW. Bounded sample ~10-40 s."""
+    from oracle import comet_oracle as O
+    from comet_amd.config import instantiate, load_config
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    cfg = load_config()
+    torch.manual_seed(0)
+    m = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg)
+    P = {k: v.detach() for k, v in m.state_dict().items()}
+    names = [k for k, p in m.named_parameters() if p.requires_grad]
+    del m
+    g = torch.Generator().manual_seed(1)
+    img = torch.randn(1, T, 3, S_img, S_img, generator=g)
+    tracks = (torch.rand(1, 1, N, 2, generator=g) * (S_img - 1)).expand(1, T, N, 2).contiguous()
+    q = torch.randn(T, 4, generator=g)
+    q = q / q.norm(dim=-1, keepdim=True)
+    gt = {"R": torch.where(q[:, :1] < 0, -q, q), "T_uvz": torch.stack([300 + torch.rand(T) * 20, 240 + torch.rand(T) * 20,
+                                                                       5 + torch.rand(T) * 10], -1),
+          "T": torch.randn(T, 3), "focal_length": torch.full((T, 2), 268.44), "ratio": torch.tensor([0.5], dtype=torch.float64)}
+    t0 = time.perf_counter()
+    O.train_step(names, P, img, tracks, gt)
+    dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": 1.0 / dt, "unit": "sequences/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"1 sequence (B=1, T={T}, {S_img}x{S_img}, N={N}) train step fwd+bwd+clip+AdamW, fp32, "
+                      f"oracle/comet_oracle.py, {dt:.1f} s, host '{cpu}'"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cpu_baseline_only:
+        print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks)))
+        return
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.frames, args.image, args.tracks)
+        torch.set_num_threads(max(1, min(8, os.cpu_count() or 1)))
+
+    import torch.distributed as dist
+    from comet_amd import functional as F
+    from comet_amd.config import instantiate, load_config
+    from comet_amd.ddp import GradBucketer
+    from comet_amd.profiler import PROF
+    from comet_amd.train import build_optimizer, train_step
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    cfg = load_config()
+    torch.manual_seed(0)  # identical random-init weights on every rank
+    model = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg).to(dev)
+    opt, sched = build_optimizer(cfg, model, iters_per_epoch=1000)
+    ddp = GradBucketer(model.camera_predictor.parameters()) if world > 1 else None
+    B, T = args.batch, args.frames
+    img, tracks, cams = synthetic(B, T, args.image, args.tracks, dev, seed=1 + rank)
+
+    def step():
+        with F.precision(torch.bfloat16):
+            return train_step(model, img, cams, tracks, opt, sched, cfg, ddp=ddp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    PROF.enabled = True
+    PROF.reset()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss, _ = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    PROF.enabled = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    prof = PROF.summary()
+    if rank == 0:
+        seqs = B * world * args.steps
+        value = seqs / elapsed
+        # dominant kernel = largest total device time among profiled entry points
+        dom_name = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
+        roof = None
+        if dom_name:
+            d = prof[dom_name]
+            avg_ms = d["ms"] / d["launches"]
+            ach = (d["flops"] / d["launches"]) / (avg_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "kernel": dom_name, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                    "launches_per_step": d["launches"] / args.steps, "avg_launch_ms": round(avg_ms, 4),
+                    "share_of_step": round(d["ms"] / (elapsed * 1e3), 3)}
+        kernels = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] / args.steps,
+                       "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["ms"] > 0 else None}
+                   for k, v in prof.items()}
+        out = {
+            "metric": "sequences/sec (BxT frames) COMET fwd+bwd, T=16 512^2",
+            "value": round(value, 4), "unit": "sequences/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) frames, U[0,511] tracks, random unit quaternions); random-init weights",
+            "config": {"workload": "train_e2epose2.py fwd+bwd (BASELINE configs[2]): COMET tracker+DINOv2+head, loss, backward, "
+                                   "grad all-reduce, clip 1.0, AdamW", "global_batch": B * world, "seq_len": T,
+                       "image": args.image, "tracks": args.tracks, "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "final_loss": float(loss.item()) if loss is not None else None,
+            "algorithmic_tflop_per_seq": 7.4773,
+            "model_tflops": round(7.4773 * value, 2),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

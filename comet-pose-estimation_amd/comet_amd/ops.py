@@ -8,6 +8,7 @@ import ctypes
 import torch
 
 from . import _lib as L
+from .profiler import PROF
 
 _DT = {torch.float32: L.F32, torch.bfloat16: L.BF16}
 
@@ -65,7 +66,9 @@ def gemm_raw(a, b, c, *, m, n, k, layout_a, lda, layout_b, ldb, ldc, batch=(1, 1
     g.aux, g.ldaux = _p(aux), ldaux
     g.stride_aux[0], g.stride_aux[1] = stride_aux
     g.alpha, g.beta, g.act = alpha, beta, act
+    e0 = PROF.start()
     L.check(L.load().comet_gemm(ctypes.byref(g), stream()), "comet_gemm")
+    PROF.stop(e0, "comet_gemm", 2.0 * m * n * k * batch[0] * batch[1])
     return c
 
 
@@ -187,7 +190,9 @@ def attention(q, k, v, heads, scale=None, out=None, lse=False):
     a.v, a.sv_b, a.sv_h, a.sv_l = _p(v), v.stride(0), D, v.stride(1)
     a.o, a.so_b, a.so_h, a.so_l = _p(out), out.stride(0), D, out.stride(1)
     a.lse, a.scale = _p(lse_t), float(scale)
+    e0 = PROF.start()
     L.check(L.load().comet_attention_fwd(ctypes.byref(a), stream()), "attention")
+    PROF.stop(e0, "comet_attention_fwd", 4.0 * B * heads * Lq * Lk * D)
     return (out, lse_t) if lse else out
 
 

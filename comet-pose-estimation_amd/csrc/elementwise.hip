@@ -144,12 +144,13 @@ extern "C" int comet_act_bwd(int act, int dtype_pre, int dtype_dy, const void* p
   const unsigned g = grid_for(n);
 #define AB(TP, TD, TX) \
   hipLaunchKernelGGL((act_bwd_kernel<TP, TD, TX>), dim3(g), dim3(256), 0, s, act, (const TP*)pre, (const TD*)dy, (TX*)dx, n)
-  if (dtype_pre == COMET_F32 && dtype_dy == COMET_F32 && dtype_dx == COMET_F32) AB(float, float, float);
-  else if (dtype_pre == COMET_BF16 && dtype_dy == COMET_F32 && dtype_dx == COMET_BF16) AB(__bf16, float, __bf16);
-  else if (dtype_pre == COMET_BF16 && dtype_dy == COMET_BF16 && dtype_dx == COMET_BF16) AB(__bf16, __bf16, __bf16);
-  else if (dtype_pre == COMET_BF16 && dtype_dy == COMET_F32 && dtype_dx == COMET_F32) AB(__bf16, float, float);
-  else if (dtype_pre == COMET_F32 && dtype_dy == COMET_F32 && dtype_dx == COMET_BF16) AB(float, float, __bf16);
-  else { set_error("comet_act_bwd: unsupported dtype combination"); return COMET_EINVAL; }
+#define AB_X(TP, TD) \
+  do { if (dtype_dx == COMET_F32) AB(TP, TD, float); else AB(TP, TD, __bf16); } while (0)
+#define AB_D(TP) \
+  do { if (dtype_dy == COMET_F32) AB_X(TP, float); else AB_X(TP, __bf16); } while (0)
+  if (dtype_pre == COMET_F32) AB_D(float); else AB_D(__bf16);
+#undef AB_D
+#undef AB_X
 #undef AB
   COMET_CHECK_LAUNCH("comet_act_bwd");
   return COMET_OK;
