@@ -62,8 +62,11 @@ def cpu_baseline(T, S_img, N):
     sequence (B=1), full train step fwd + bwd + clip + AdamW. Bounded sample ~10-40 s."""
     from oracle import comet_oracle as O
     from comet_amd.config import instantiate, load_config
-    threads = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if threads <= 0:
+        threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     torch.set_num_threads(threads)
+    print(f"[bench] cpu baseline: oracle train step on {threads} threads ...", file=sys.stderr, flush=True)
     cfg = load_config()
     torch.manual_seed(0)
     m = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg)
