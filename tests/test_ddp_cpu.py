@@ -1,0 +1,109 @@
+"""World-size-2 gloo tests of the data-parallel gradient exchange (comet_amd/ddp.py), CPU only.
+
+Checks what DistributedDataParallel guarantees for the reference (train_e2epose2.py:83): after
+backward every rank holds the mean of the per-rank gradients, parameters that took no part in the
+loss keep grad=None, and the buckets are re-armed every step.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class _Net(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.a = torch.nn.Linear(16, 32)
+        self.b = torch.nn.Linear(32, 32)
+        self.unused = torch.nn.Linear(32, 8)  # never executed, like FeatureFusion in the head
+        self.c = torch.nn.Linear(32, 4)
+
+    def forward(self, x):
+        return self.c(torch.relu(self.b(torch.relu(self.a(x)))))
+
+
+def _data(rank, step):
+    g = torch.Generator().manual_seed(100 * step + rank)
+    return torch.randn(8, 16, generator=g), torch.randn(8, 4, generator=g)
+
+
+def _worker(rank, world, port, bucket_mb, q, paths):
+    import sys
+    sys.path[:0] = paths
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from comet_amd.ddp import GradBucketer
+        net = _Net()
+        bk = GradBucketer(net.parameters(), bucket_mb=bucket_mb)
+        out = []
+        for step in range(2):
+            bk.prepare_backward()
+            x, y = _data(rank, step)
+            loss = ((net(x) - y) ** 2).mean()
+            loss.backward()
+            bk.finish_backward()
+            out.append({k: (None if p.grad is None else p.grad.detach().numpy().copy()) for k, p in net.named_parameters()})
+        q.put((rank, len(bk.buckets), out))
+    finally:
+        dist.destroy_process_group()
+
+
+def _expected(world):
+    net = _Net()
+    res = []
+    for step in range(2):
+        acc = {k: torch.zeros_like(p) for k, p in net.named_parameters()}
+        for r in range(world):
+            net.zero_grad(set_to_none=True)
+            x, y = _data(r, step)
+            ((net(x) - y) ** 2).mean().backward()
+            for k, p in net.named_parameters():
+                if p.grad is not None:
+                    acc[k] += p.grad / world
+        res.append(acc)
+    return res
+
+
+@pytest.mark.parametrize("bucket_mb", [64, 0.004])  # one bucket / several buckets
+def test_bucketed_allreduce_matches_mean_grad(bucket_mb):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, bucket_mb, q, [ROOT, PKG])) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        rank, nb, out = q.get(timeout=120)
+        results[rank] = (nb, out)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = _expected(world)
+    if bucket_mb < 1:
+        assert results[0][0] > 1
+    for rank in range(world):
+        for step in range(2):
+            got = results[rank][1][step]
+            for k, g in got.items():
+                if k.startswith("unused."):
+                    assert g is None, k
+                else:
+                    torch.testing.assert_close(torch.from_numpy(g), exp[step][k], rtol=1e-5, atol=1e-6)
