@@ -28,6 +28,20 @@ class GemmArgs(ctypes.Structure):
         ("resid", c_vp), ("ldr", c_i64), ("stride_r", c_i64 * 2),
         ("aux", c_vp), ("ldaux", c_i64), ("stride_aux", c_i64 * 2),
         ("alpha", ctypes.c_float), ("beta", ctypes.c_float), ("act", c_i32),
+        ("workspace", c_vp), ("workspace_bytes", c_i64), ("split_k", c_i32),
+    ]
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", c_i32), ("dtype_y", c_i32),
+        ("x", c_vp), ("n", c_i64), ("h", c_i64), ("w", c_i64), ("c", c_i64),
+        ("weight", c_vp), ("cout", c_i64), ("ldw", c_i64),
+        ("kh", c_i32), ("kw", c_i32), ("stride", c_i32), ("pad", c_i32),
+        ("bias", c_vp),
+        ("y", c_vp), ("ldy", c_i64),
+        ("resid", c_vp), ("ldr", c_i64), ("beta", ctypes.c_float),
+        ("act", c_i32),
     ]
 
 
@@ -50,6 +64,8 @@ SIGNATURES = {
     "comet_version": (_INT, []),
     "comet_last_error": (ctypes.c_char_p, []),
     "comet_gemm": (_INT, [ctypes.POINTER(GemmArgs), c_vp]),
+    "comet_gemm_workspace": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64)]),
+    "comet_conv2d_nhwc": (_INT, [ctypes.POINTER(ConvArgs), c_vp]),
     "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _F, _INT, c_vp]),
     "comet_layernorm_bwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, _INT, c_vp]),
     "comet_attention_fwd": (_INT, [ctypes.POINTER(AttnArgs), c_vp]),
@@ -63,7 +79,8 @@ SIGNATURES = {
     "comet_sq_norm_multi": (_INT, [c_vp, c_vp, _INT, c_vp, c_vp]),
     "comet_adamw_multi": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, _INT, _F, _F, _F, _F, _F, _INT, c_vp, _F, c_vp]),
     "comet_im2col_nhwc": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _INT, _INT, _INT, _INT, c_i64, c_i64, c_i64, c_vp]),
-    "comet_instnorm_nhwc": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, _F, _INT, _INT, c_vp]),
+    "comet_instnorm_workspace": (_INT, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),
+    "comet_instnorm_nhwc": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, _F, _INT, _INT, c_vp, c_i64, c_vp]),
     "comet_resize_bilinear": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, _INT, c_vp]),
     "comet_act_fwd": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_vp]),
     "comet_binary": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_i64, c_vp]),

@@ -94,6 +94,8 @@ def conv2d_nhwc(x, conv, stride, pad, out_dtype=None):
         y = F.linear(x.reshape(-1, c), wm, conv.bias, out_dtype=out_dtype)
         return y.reshape(n, h, wd, cout)
     xc = x if x.dtype == wm.dtype else ops.cast(x, wm.dtype)
+    if wm.dtype == torch.bfloat16 and cin % 8 == 0:  # implicit GEMM: no im2col matrix in HBM
+        return ops.conv2d_nhwc(xc, wm, kh, kw, stride, pad, bias=conv.bias, out_dtype=out_dtype or wm.dtype)
     cols, oh, ow = ops.im2col_nhwc(xc, kh, kw, stride, pad, out_dtype=wm.dtype, ldc=wm.shape[1])
     y = F.linear(cols, wm, conv.bias, out_dtype=out_dtype)
     return y.reshape(x.shape[0], oh, ow, cout)

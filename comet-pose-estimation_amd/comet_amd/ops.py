@@ -40,7 +40,7 @@ def _req_cuda(*ts):
 def gemm_raw(a, b, c, *, m, n, k, layout_a, lda, layout_b, ldb, ldc, batch=(1, 1),
              stride_a=(0, 0), stride_b=(0, 0), stride_c=(0, 0), bias=None, bias_mode=0,
              stride_bias=(0, 0), resid=None, ldr=0, stride_r=(0, 0), beta=1.0, aux=None,
-             ldaux=0, stride_aux=(0, 0), alpha=1.0, act=L.ACT_NONE):
+             ldaux=0, stride_aux=(0, 0), alpha=1.0, act=L.ACT_NONE, split_k=0):
     _req_cuda(a, b, c, bias, resid, aux)
     if a.dtype != b.dtype:
         raise L.CometHipError("gemm: A and B must share a dtype")
@@ -66,9 +66,22 @@ def gemm_raw(a, b, c, *, m, n, k, layout_a, lda, layout_b, ldb, ldc, batch=(1, 1
     g.aux, g.ldaux = _p(aux), ldaux
     g.stride_aux[0], g.stride_aux[1] = stride_aux
     g.alpha, g.beta, g.act = alpha, beta, act
+    g.split_k = split_k
+    lib = L.load()
+    ws_bytes = ctypes.c_int64(0)
+    L.check(lib.comet_gemm_workspace(ctypes.byref(g), ctypes.byref(ws_bytes)), "comet_gemm_workspace")
+    ws = None
+    if ws_bytes.value > 0:  # split-K partials (torch caching allocator: no device sync)
+        ws = torch.empty((ws_bytes.value + 3) // 4, device=c.device, dtype=torch.float32)
+        g.workspace, g.workspace_bytes = ws.data_ptr(), ws_bytes.value
     e0 = PROF.start()
-    L.check(L.load().comet_gemm(ctypes.byref(g), stream()), "comet_gemm")
-    PROF.stop(e0, "comet_gemm", 2.0 * m * n * k * batch[0] * batch[1])
+    L.check(lib.comet_gemm(ctypes.byref(g), stream()), "comet_gemm")
+    if e0 is not None:
+        name = "comet_gemm"
+        if PROF.detail:
+            name = (f"gemm L{layout_a}{layout_b} {a.dtype}->{c.dtype} M{m} N{n} K{k} b{batch[0]}x{batch[1]}"
+                    f" act{act}{' bias' if bias is not None else ''}{' res' if resid is not None else ''}")
+        PROF.stop(e0, name, 2.0 * m * n * k * batch[0] * batch[1])
     return c
 
 
@@ -224,6 +237,36 @@ def colsum(x2d, out=None, accumulate=False):
     return out
 
 
+def conv2d_nhwc(x, w, kh, kw, stride, pad, bias=None, act=L.ACT_NONE, resid=None, beta=1.0, out=None,
+                out_dtype=None):
+    """Implicit-GEMM conv (comet_conv2d_nhwc). x [n,h,w,c] bf16 (c % 8 == 0), w [cout, ldw] bf16 with
+    columns (ky, kx, ci). Returns y [n, oh, ow, cout]."""
+    _req_cuda(x, w, bias, resid)
+    n, h, wd, c = x.shape
+    cout = w.shape[0]
+    oh = (h + 2 * pad - kh) // stride + 1
+    ow = (wd + 2 * pad - kw) // stride + 1
+    if not x.is_contiguous():
+        x = x.contiguous()
+    if out is None:
+        out = torch.empty(n, oh, ow, cout, device=x.device, dtype=out_dtype or x.dtype)
+    a = L.ConvArgs()
+    a.dtype, a.dtype_y = dt(x), dt(out)
+    a.x, a.n, a.h, a.w, a.c = _p(x), n, h, wd, c
+    a.weight, a.cout, a.ldw = _p(w), cout, w.stride(0)
+    a.kh, a.kw, a.stride, a.pad = kh, kw, stride, pad
+    a.bias = _p(bias)
+    a.y, a.ldy = _p(out), cout
+    a.resid, a.ldr, a.beta = _p(resid), (cout if resid is not None else 0), beta
+    a.act = act
+    e0 = PROF.start()
+    L.check(L.load().comet_conv2d_nhwc(ctypes.byref(a), stream()), "comet_conv2d_nhwc")
+    if e0 is not None:
+        name = f"conv {kh}x{kw}s{stride} c{c}->{cout} {h}x{wd} n{n}" if PROF.detail else "comet_conv2d_nhwc"
+        PROF.stop(e0, name, 2.0 * n * oh * ow * cout * kh * kw * c)
+    return out
+
+
 def im2col_nhwc(x, kh, kw, stride, pad, out_dtype=None, ldc=None):
     n, h, w, c = x.shape
     oh = (h + 2 * pad - kh) // stride + 1
@@ -239,8 +282,12 @@ def im2col_nhwc(x, kh, kw, stride, pad, out_dtype=None, ldc=None):
 def instnorm_nhwc(x, res=None, relu=False, eps=1e-5, out=None, relu_inner=False):
     n, h, w, c = x.shape
     out = out if out is not None else torch.empty_like(x)
-    L.check(L.load().comet_instnorm_nhwc(dt(x), _p(x), _p(res), _p(out), n, h * w, c, float(eps),
-                                         int(relu), int(relu_inner), stream()), "instnorm")
+    lib = L.load()
+    nb = ctypes.c_int64(0)
+    L.check(lib.comet_instnorm_workspace(n, h * w, c, ctypes.byref(nb)), "instnorm_workspace")
+    ws = torch.empty((nb.value + 3) // 4, device=x.device, dtype=torch.float32) if nb.value else None
+    L.check(lib.comet_instnorm_nhwc(dt(x), _p(x), _p(res), _p(out), n, h * w, c, float(eps),
+                                    int(relu), int(relu_inner), _p(ws), nb.value, stream()), "instnorm")
     return out
 
 

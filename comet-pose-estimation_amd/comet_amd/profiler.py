@@ -10,6 +10,7 @@ import torch
 class _Prof:
     def __init__(self):
         self.enabled = False
+        self.detail = False  # key GEMM records by shape/layout (tools/gemm_shapes.py)
         self.records = []
         self._pool = []
 

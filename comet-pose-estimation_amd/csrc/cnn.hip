@@ -66,6 +66,43 @@ __global__ void resize_kernel(const TI* __restrict__ x, TO* __restrict__ y, int 
   }
 }
 
+// NHWC with c % 8 == 0: one thread per (output pixel, 8 channels), 16-B (bf16) loads/stores.
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+resize_nhwc8_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n, int c, int h, int w,
+                    int oh, int ow, int add) {
+  const int cg8 = c / 8;
+  const int64_t total = n * oh * ow * cg8;
+  const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gs) {
+    const int cg = (int)(i % cg8);
+    const int64_t pix = i / cg8;
+    const int ox = (int)(pix % ow);
+    const int64_t t = pix / ow;
+    const int oy = (int)(t % oh);
+    const int64_t ni = t / oh;
+    int64_t y0, y1, x0, x1;
+    float fy, fx;
+    ac_coord(oy, h, oh, y0, y1, fy);
+    ac_coord(ox, w, ow, x0, x1, fx);
+    const TI* b = x + ni * h * w * c + cg * 8;
+    float v00[8], v01[8], v10[8], v11[8];
+    load8(b + (y0 * w + x0) * c, v00);
+    load8(b + (y0 * w + x1) * c, v01);
+    load8(b + (y1 * w + x0) * c, v10);
+    load8(b + (y1 * w + x1) * c, v11);
+    float o[8];
+    TO* yo = y + pix * c + cg * 8;
+    if (add) load8(yo, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (1.f - fy) * ((1.f - fx) * v00[e] + fx * v01[e]) + fy * ((1.f - fx) * v10[e] + fx * v11[e]);
+      o[e] = add ? o[e] + v : v;
+    }
+    store8(yo, o);
+  }
+}
+
 inline unsigned g1d(int64_t n) {
   int64_t g = cdiv(n, 256);
   return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
@@ -98,6 +135,17 @@ extern "C" int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, cons
                                      int64_t ow, int add, void* stream) {
   COMET_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "comet_resize_bilinear: bad args");
   hipStream_t s = as_stream(stream);
+  if (nhwc && c % 8 == 0 && ((uintptr_t)x | (uintptr_t)y) % 32 == 0 && h < (1 << 30) && w < (1 << 30)) {
+    const unsigned g8 = g1d(n * oh * ow * (c / 8));
+#define RS8(TI, TO) hipLaunchKernelGGL((resize_nhwc8_kernel<TI, TO>), dim3(g8), dim3(256), 0, s, (const TI*)x, (TO*)y, n, (int)c, (int)h, (int)w, (int)oh, (int)ow, add)
+    if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RS8(float, float);
+    else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) RS8(float, __bf16);
+    else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) RS8(__bf16, __bf16);
+    else RS8(__bf16, float);
+#undef RS8
+    COMET_CHECK_LAUNCH("comet_resize_bilinear");
+    return COMET_OK;
+  }
   const unsigned g = g1d(n * c * oh * ow);
 #define RS(TI, TO) hipLaunchKernelGGL((resize_kernel<TI, TO>), dim3(g), dim3(256), 0, s, (const TI*)x, (TO*)y, nhwc, n, c, h, w, oh, ow, add)
   if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RS(float, float);

@@ -1,15 +1,28 @@
 // Batched MFMA GEMM with fused bias / activation / residual epilogue (comet_gemm).
 //
 // Replaces nn.Linear / MHA in_proj+out_proj / conv-after-im2col of the reference
-// (modules.py:119-154, 248-344; blocks.py:27-348; camera_predictor10.py:75-87,126-280).
+// (modules.py:119-154, 248-344; blocks.py:27-348; camera_predictor10.py:75-87,126-280) and the
+// head's backward GEMMs (dX = dY.W, dW = dY^T.X).
 //
 // Tile 128x128, 256 threads = 4 waves (2x2), each wave owns 64x64 = 4x4 MFMA 16x16 tiles.
-//  bf16: v_mfma_f32_16x16x32_bf16, BK = 32   (lane l: A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15])
-//  f32 : v_mfma_f32_16x16x4_f32,  BK = 16   (lane reads 4 consecutive k; instruction e uses
-//        k = 4(l>>4)+e for A and B alike, so one ds_read_b128 feeds 4 MFMAs)
-// LDS holds both operands k-contiguous ([row][BK+pad]); row pitch 80 B keeps the 16-lane
-// ds_read_b128 groups conflict-free. Global->register loads of tile t+1 are issued before the
-// MFMAs of tile t and written to the other LDS buffer afterwards (one barrier per k-tile).
+//
+// bf16 kernel: v_mfma_f32_16x16x32_bf16, BK = 64 (two 32-deep MFMA steps per k-tile).
+//   Each operand keeps the LDS image its global layout gives for free:
+//   * k-contiguous (layout 0): [128 rows][64 k + 8 pad]   (144-B pitch: ds_read_b128, conflict-free)
+//   * row-contiguous (layout 1): [64 k][128 rows + 16 pad] (288-B pitch), fragments read with
+//     ds_read_b64_tr_b16 (lane gets 4 k of one row per read, two reads = the 8 k of a fragment).
+//     k rows are stored with bits 2 and 3 of k swapped so the 8 rows one half-wave reads fall on
+//     8 distinct 32-B bank groups.
+//   Global -> register staging, write of tile t+1 after the barrier of tile t-1, loads of tile t+2
+//   issued right after (one barrier per k-tile).
+// f32 kernel (parity precision): v_mfma_f32_16x16x4_f32, BK = 16, both operands k-contiguous in LDS.
+//
+// Split-K: when the output has fewer tiles than the chip has CUs and K is long (the weight-gradient
+// GEMMs: K = all tokens of the batch), blockIdx.z splits K; every split writes an f32 partial tile
+// into the caller's workspace and a second kernel sums the splits in a fixed order (deterministic)
+// and applies the epilogue.
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace comet {
@@ -18,152 +31,320 @@ namespace {
 
 constexpr int BM = 128, BN = 128, NT = 256;
 
-template <typename T> struct Cfg;
-template <> struct Cfg<__bf16> { static constexpr int BK = 32, VEC = 8, PAD = 8; };
-template <> struct Cfg<float>  { static constexpr int BK = 16, VEC = 4, PAD = 4; };
-
-template <typename T> struct VecT;
-template <> struct VecT<__bf16> { typedef uint4 type; };   // 8 x bf16
-template <> struct VecT<float>  { typedef float4 type; };  // 4 x f32
-
 struct Epi {
   const float* bias; int bias_mode; int64_t sb0, sb1;
   const void* resid; int64_t ldr, sr0, sr1; float beta;
   void* aux; int64_t ldaux, sx0, sx1;
   float alpha; int act;
+  int vec;  // output / resid / aux rows allow 8-wide vector access (host-checked)
 };
 
-// Load one operand tile (ROWS x BK of the k-contiguous LDS image) from global into registers.
-// layout 0: element (r, k) at base[r*ld + k]; layout 1: at base[k*ld + r].
-template <typename T, int LAYOUT, bool VEC>
-struct TileLoader {
-  static constexpr int BK = Cfg<T>::BK, V = Cfg<T>::VEC;
-  static constexpr int NV = 128 * BK / V / NT;  // vectors per thread (=2)
-  typedef typename VecT<T>::type vec_t;
-  vec_t reg[NV];
-
-  __device__ __forceinline__ void load(const T* __restrict__ base, int64_t ld, int64_t r0,
-                                       int64_t rmax, int64_t k0, int64_t kmax) {
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = tid + i * NT;
-      T tmp[V];
-      if (LAYOUT == 0) {
-        const int row = v / (BK / V), kv = (v % (BK / V)) * V;
-        const int64_t gr = r0 + row, gk = k0 + kv;
-        if (VEC) {
-          if (gr < rmax && gk < kmax) {
-            reg[i] = *reinterpret_cast<const vec_t*>(base + gr * ld + gk);
-          } else {
-            reg[i] = vec_t{};
-          }
-          continue;
-        }
-#pragma unroll
-        for (int e = 0; e < V; ++e)
-          tmp[e] = (gr < rmax && gk + e < kmax) ? base[gr * ld + gk + e] : T(0.f);
-      } else {
-        const int krow = v / (128 / V), rv = (v % (128 / V)) * V;
-        const int64_t gk = k0 + krow, gr = r0 + rv;
-        if (VEC) {
-          if (gk < kmax && gr < rmax) {
-            reg[i] = *reinterpret_cast<const vec_t*>(base + gk * ld + gr);
-          } else {
-            reg[i] = vec_t{};
-          }
-          continue;
-        }
-#pragma unroll
-        for (int e = 0; e < V; ++e)
-          tmp[e] = (gk < kmax && gr + e < rmax) ? base[gk * ld + gr + e] : T(0.f);
-      }
-      reg[i] = *reinterpret_cast<vec_t*>(tmp);
-    }
-  }
-
-  __device__ __forceinline__ void store(T* __restrict__ lds) const {
-    constexpr int LDW = BK + Cfg<T>::PAD;
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = tid + i * NT;
-      if (LAYOUT == 0) {
-        const int row = v / (BK / V), kv = (v % (BK / V)) * V;
-        *reinterpret_cast<vec_t*>(lds + row * LDW + kv) = reg[i];
-      } else {
-        const int krow = v / (128 / V), rv = (v % (128 / V)) * V;
-        const T* t = reinterpret_cast<const T*>(&reg[i]);
-#pragma unroll
-        for (int e = 0; e < V; ++e) lds[(rv + e) * LDW + krow] = t[e];
-      }
-    }
-  }
+// Split-K partials: ws[((z * nb) + bz) * M * N + row * N + col], f32.
+struct Split {
+  float* ws; int64_t kchunk;  // k range of split z: [z*kchunk, min(K, (z+1)*kchunk))
 };
 
-template <typename T>
-__device__ __forceinline__ void mma_tile(const T* __restrict__ As, const T* __restrict__ Bs,
-                                         f32x4 (&acc)[4][4], int wm, int wn, int lane);
-
-template <>
-__device__ __forceinline__ void mma_tile<__bf16>(const __bf16* __restrict__ As,
-                                                 const __bf16* __restrict__ Bs,
-                                                 f32x4 (&acc)[4][4], int wm, int wn, int lane) {
-  constexpr int LDW = 32 + 8;
-  bf16x8 a[4], b[4];
-  const int r = lane & 15, kq = (lane >> 4) * 8;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + r) * LDW + kq);
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 16 + r) * LDW + kq);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+template <typename TC>
+__device__ __forceinline__ void epi_store(const Epi& epi, TC* __restrict__ C, int64_t ldc,
+                                          const TC* R, TC* X, const float* bias,
+                                          int64_t row, int64_t col, float acc) {
+  float v = epi.alpha * acc;
+  if (bias) v += epi.bias_mode == 1 ? bias[col] : bias[row];
+  if (X) X[row * epi.ldaux + col] = from_f32<TC>(v);
+  v = apply_act(epi.act, v);
+  if (R) v += epi.beta * to_f32(R[row * epi.ldr + col]);
+  C[row * ldc + col] = from_f32<TC>(v);
 }
 
-template <>
-__device__ __forceinline__ void mma_tile<float>(const float* __restrict__ As,
-                                                const float* __restrict__ Bs,
-                                                f32x4 (&acc)[4][4], int wm, int wn, int lane) {
-  constexpr int LDW = 16 + 4;
-  f32x4 a[4], b[4];
-  const int r = lane & 15, kq = (lane >> 4) * 4;
+// Write the 128x128 accumulator tile: either the fused epilogue or the raw split-K partial.
+template <typename TC, bool SPLIT>
+__device__ __forceinline__ void write_tile(const f32x4 (&acc)[4][4], const Epi& epi, TC* __restrict__ C,
+                                           int64_t ldc, int64_t b0, int64_t b1, int64_t bz,
+                                           int64_t m0, int64_t n0, int64_t M, int64_t N,
+                                           const Split& sp, int wm, int wn, int lane) {
+  const int cl = lane & 15, rq = (lane >> 4) * 4;
+  if (SPLIT) {
+    float* W = sp.ws + ((int64_t)blockIdx.z * gridDim.y + bz) * M * N;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    a[i] = *reinterpret_cast<const f32x4*>(As + (wm * 64 + i * 16 + r) * LDW + kq);
+    for (int j = 0; j < 4; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 16 + cl;
+      if (col >= N) continue;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    b[j] = *reinterpret_cast<const f32x4*>(Bs + (wn * 64 + j * 16 + r) * LDW + kq);
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm * 64 + i * 16 + rq + r;
+          if (row < M) W[row * N + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  const TC* R = epi.resid ? reinterpret_cast<const TC*>(epi.resid) + b0 * epi.sr0 + b1 * epi.sr1 : nullptr;
+  TC* X = epi.aux ? reinterpret_cast<TC*>(epi.aux) + b0 * epi.sx0 + b1 * epi.sx1 : nullptr;
+  const float* bias = epi.bias ? epi.bias + b0 * epi.sb0 + b1 * epi.sb1 : nullptr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t col = n0 + wn * 64 + j * 16 + cl;
+    if (col >= N) continue;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm * 64 + i * 16 + rq + r;
+        if (row < M) epi_store<TC>(epi, C, ldc, R, X, bias, row, col, acc[i][j][r]);
+      }
+  }
 }
 
-template <typename T, typename TC, int LA, int LB, bool VA, bool VB>
-__global__ void __launch_bounds__(NT)
-gemm_kernel(const T* __restrict__ A, int64_t lda, int64_t sa0, int64_t sa1,
-            const T* __restrict__ B, int64_t ldb, int64_t sb0, int64_t sb1,
-            TC* __restrict__ C, int64_t ldc, int64_t sc0, int64_t sc1,
-            int64_t M, int64_t N, int64_t K, int64_t nb1, int tiles_n, Epi epi) {
-  constexpr int BK = Cfg<T>::BK, LDW = BK + Cfg<T>::PAD;
-  __shared__ __attribute__((aligned(16))) T smem[2][2][128 * LDW];
+// Epilogue through LDS (bf16 kernel): the 128x128 f32 accumulator tile is parked in LDS, then each
+// thread owns 8 consecutive columns of 8 rows, so bias / residual / aux / output move as 16-B
+// (bf16) or 32-B (f32) vectors instead of 2-4-B column-strided scalars.
+constexpr int CP = 132;  // f32 pitch of the parked tile: conflict-free fragment writes
 
-  const int nwg = gridDim.x;
-  const int tile = xcd_remap(blockIdx.x, nwg);
+template <typename TC, bool SPLIT>
+__device__ __forceinline__ void write_tile_lds(const f32x4 (&acc)[4][4], float* __restrict__ cs,
+                                               const Epi& epi, TC* __restrict__ C, int64_t ldc,
+                                               int64_t b0, int64_t b1, int64_t bz, int64_t m0, int64_t n0,
+                                               int64_t M, int64_t N, const Split& sp, int wm, int wn, int lane) {
+  const int cl = lane & 15, rq = (lane >> 4) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cs[(wm * 64 + i * 16 + rq + r) * CP + wn * 64 + j * 16 + cl] = acc[i][j][r];
+  __syncthreads();
+  const int t = threadIdx.x, cg = t & 15, rb = t >> 4;
+  const int64_t col0 = n0 + cg * 8;
+  if (col0 >= N) return;
+  const bool full = epi.vec && col0 + 8 <= N;
+  if (SPLIT) {
+    float* W = sp.ws + ((int64_t)blockIdx.z * gridDim.y + bz) * M * N;
+#pragma unroll 2
+    for (int q = 0; q < 8; ++q) {
+      const int64_t row = m0 + rb + 16 * q;
+      if (row >= M) break;
+      float v[8];
+      load8(cs + (rb + 16 * q) * CP + cg * 8, v);
+      if (full) {
+        store8(W + row * N + col0, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (col0 + e < N) W[row * N + col0 + e] = v[e];
+      }
+    }
+    return;
+  }
+  const TC* R = epi.resid ? reinterpret_cast<const TC*>(epi.resid) + b0 * epi.sr0 + b1 * epi.sr1 : nullptr;
+  TC* X = epi.aux ? reinterpret_cast<TC*>(epi.aux) + b0 * epi.sx0 + b1 * epi.sx1 : nullptr;
+  const float* bias = epi.bias ? epi.bias + b0 * epi.sb0 + b1 * epi.sb1 : nullptr;
+  float bc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bc[e] = (bias && epi.bias_mode == 1 && col0 + e < N) ? bias[col0 + e] : 0.f;
+#pragma unroll 2
+  for (int q = 0; q < 8; ++q) {
+    const int64_t row = m0 + rb + 16 * q;
+    if (row >= M) break;
+    float v[8];
+    load8(cs + (rb + 16 * q) * CP + cg * 8, v);
+    const float br = (bias && epi.bias_mode == 2) ? bias[row] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = epi.alpha * v[e] + bc[e] + br;
+    if (full) {
+      if (X) store8(X + row * epi.ldaux + col0, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = apply_act(epi.act, v[e]);
+      if (R) {
+        float r[8];
+        load8(R + row * epi.ldr + col0, r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += epi.beta * r[e];
+      }
+      store8(C + row * ldc + col0, v);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int64_t col = col0 + e;
+        if (col >= N) break;
+        float o = v[e];
+        if (X) X[row * epi.ldaux + col] = from_f32<TC>(o);
+        o = apply_act(epi.act, o);
+        if (R) o += epi.beta * to_f32(R[row * epi.ldr + col]);
+        C[row * ldc + col] = from_f32<TC>(o);
+      }
+    }
+  }
+}
+
+// ============================== bf16 kernel ===============================================
+namespace bf {
+constexpr int BK = 64;
+constexpr int P0 = BK + 8;       // layout-0 image pitch (elements)
+constexpr int P1 = 128 + 16;     // layout-1 image pitch (elements)
+constexpr int IMG = 128 * P0;    // == 64 * P1 == 9216 elements per operand per stage
+static_assert(128 * P0 == 64 * P1, "image sizes");
+static_assert(2 * 2 * IMG * 2 >= 128 * CP * 4, "parked C tile must fit in the staging LDS");
+
+__device__ __forceinline__ int krow_phys(int k) { return (k & ~12) | ((k >> 1) & 4) | ((k << 1) & 8); }
+
+__device__ __forceinline__ uint4 pack8(const unsigned short (&s)[8]) {
+  uint4 u;
+  u.x = (unsigned)s[0] | ((unsigned)s[1] << 16);
+  u.y = (unsigned)s[2] | ((unsigned)s[3] << 16);
+  u.z = (unsigned)s[4] | ((unsigned)s[5] << 16);
+  u.w = (unsigned)s[6] | ((unsigned)s[7] << 16);
+  return u;
+}
+
+// One operand's 128 x 64 tile, 4 x 16-B vectors per thread.
+template <int LAYOUT, bool VEC>
+struct Loader {
+  uint4 reg[4];
+
+  __device__ __forceinline__ void load(const __bf16* __restrict__ base, int64_t ld, int64_t r0,
+                                       int64_t rmax, int64_t k0, int64_t kmax) {
+    const unsigned short* b16 = reinterpret_cast<const unsigned short*>(base);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (LAYOUT == 0) {
+        const int row = v >> 3, kv = (v & 7) * 8;
+        const int64_t gr = r0 + row, gk = k0 + kv;
+        if (VEC) {
+          reg[i] = (gr < rmax && gk < kmax) ? *reinterpret_cast<const uint4*>(b16 + gr * ld + gk) : uint4{0, 0, 0, 0};
+        } else {
+          unsigned short s[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s[e] = (gr < rmax && gk + e < kmax) ? b16[gr * ld + gk + e] : (unsigned short)0;
+          reg[i] = pack8(s);
+        }
+      } else {
+        const int krow = v >> 4, rv = (v & 15) * 8;
+        const int64_t gk = k0 + krow, gr = r0 + rv;
+        if (VEC) {
+          reg[i] = (gk < kmax && gr < rmax) ? *reinterpret_cast<const uint4*>(b16 + gk * ld + gr) : uint4{0, 0, 0, 0};
+        } else {
+          unsigned short s[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s[e] = (gk < kmax && gr + e < rmax) ? b16[gk * ld + gr + e] : (unsigned short)0;
+          reg[i] = pack8(s);
+        }
+      }
+    }
+  }
+
+  __device__ __forceinline__ void store(__bf16* __restrict__ img) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (LAYOUT == 0) {
+        const int row = v >> 3, kv = (v & 7) * 8;
+        *reinterpret_cast<uint4*>(img + row * P0 + kv) = reg[i];
+      } else {
+        const int krow = v >> 4, rv = (v & 15) * 8;
+        *reinterpret_cast<uint4*>(img + krow_phys(krow) * P1 + rv) = reg[i];
+      }
+    }
+  }
+};
+
+// Implicit-GEMM convolution A operand (NHWC input, k order (ky, kx, ci), c % 8 == 0): the
+// 128 x 64 tile of the virtual im2col matrix is gathered straight from the activation, 16 B
+// (8 channels of one tap) per load; padding taps and rows >= M load zeros.
+struct ConvGeo {
+  const __bf16* x; int h, w, c, kw, stride, pad, oh, ow;
+};
+
+struct ConvLoader {
+  uint4 reg[4];
+  int64_t base[4];
+  int iy0[4], ix0[4];
+  ConvGeo g;
+
+  __device__ __forceinline__ void init(const ConvGeo& geo, int64_t m0, int64_t M) {
+    g = geo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = m0 + (threadIdx.x >> 3) + 32 * i;
+      if (row < M) {
+        const int ox = (int)(row % g.ow);
+        const int64_t t = row / g.ow;
+        const int oy = (int)(t % g.oh);
+        const int64_t ni = t / g.oh;
+        iy0[i] = oy * g.stride - g.pad;
+        ix0[i] = ox * g.stride - g.pad;
+        base[i] = ni * g.h * g.w * g.c;
+      } else {
+        iy0[i] = -(1 << 29);
+        ix0[i] = 0;
+        base[i] = 0;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(const __bf16*, int64_t, int64_t, int64_t, int64_t k0, int64_t kmax) {
+    const int k = (int)k0 + (threadIdx.x & 7) * 8;
+    const int tap = k / g.c, ci = k - tap * g.c;
+    const int ky = tap / g.kw, kx = tap - ky * g.kw;
+    const unsigned short* x16 = reinterpret_cast<const unsigned short*>(g.x);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+      const bool ok = k < kmax && iy >= 0 && iy < g.h && ix >= 0 && ix < g.w;
+      reg[i] = ok ? *reinterpret_cast<const uint4*>(x16 + base[i] + ((int64_t)iy * g.w + ix) * g.c + ci)
+                  : uint4{0, 0, 0, 0};
+    }
+  }
+
+  __device__ __forceinline__ void store(__bf16* __restrict__ img) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = threadIdx.x + i * NT;
+      *reinterpret_cast<uint4*>(img + (v >> 3) * P0 + (v & 7) * 8) = reg[i];
+    }
+  }
+};
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// MFMA operand fragment: lane l gets rows rbase + (l & 15), k = s*32 + 8*(l >> 4) + 0..7.
+template <int LAYOUT>
+__device__ __forceinline__ bf16x8 frag(const __bf16* __restrict__ img, int rbase, int s, int lane) {
+  if (LAYOUT == 0) {
+    return *reinterpret_cast<const bf16x8*>(img + (rbase + (lane & 15)) * P0 + s * 32 + (lane >> 4) * 8);
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int k = s * 32 + 8 * g + q;
+    const __bf16* a0 = img + krow_phys(k) * P1 + rbase + 4 * p;
+    const __bf16* a1 = img + krow_phys(k + 4) * P1 + rbase + 4 * p;
+    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+  }
+}
+
+template <typename TC, int LA, int LB, bool VA, bool VB, bool SPLIT, bool CONV = false>
+__global__ void __launch_bounds__(NT, 2)
+gemm_bf16_kernel(const __bf16* __restrict__ A, int64_t lda, int64_t sa0, int64_t sa1,
+                 const __bf16* __restrict__ B, int64_t ldb, int64_t sb0, int64_t sb1,
+                 TC* __restrict__ C, int64_t ldc, int64_t sc0, int64_t sc1,
+                 int64_t M, int64_t N, int64_t K, int64_t nb1, int tiles_n, Epi epi, Split sp,
+                 ConvGeo geo = ConvGeo{}) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2][2][IMG];
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int64_t bz = blockIdx.y, b0 = bz / nb1, b1 = bz % nb1;
   A += b0 * sa0 + b1 * sa1;
   B += b0 * sb0 + b1 * sb1;
   C += b0 * sc0 + b1 * sc1;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  int64_t kbeg = 0, kend = K;
+  if (SPLIT) {
+    kbeg = (int64_t)blockIdx.z * sp.kchunk;
+    kend = kbeg + sp.kchunk < K ? kbeg + sp.kchunk : K;
+  }
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -174,56 +355,244 @@ gemm_kernel(const T* __restrict__ A, int64_t lda, int64_t sa0, int64_t sa1,
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  TileLoader<T, LA, VA> la;
-  TileLoader<T, LB, VB> lb;
-  const int nk = (int)((K + BK - 1) / BK);
+  typename std::conditional<CONV, ConvLoader, Loader<LA, VA>>::type la;
+  Loader<LB, VB> lb;
+  if constexpr (CONV) la.init(geo, m0, M);
+  const int nk = (int)((kend - kbeg + BK - 1) / BK);
 
-  la.load(A, lda, m0, M, 0, K);
-  lb.load(B, ldb, n0, N, 0, K);
-  la.store(smem[0][0]);
-  lb.store(smem[0][1]);
+  if (nk > 0) {
+    la.load(A, lda, m0, M, kbeg, kend);
+    lb.load(B, ldb, n0, N, kbeg, kend);
+    la.store(smem[0][0]);
+    lb.store(smem[0][1]);
+    if (nk > 1) {
+      la.load(A, lda, m0, M, kbeg + BK, kend);
+      lb.load(B, ldb, n0, N, kbeg + BK, kend);
+    }
+  }
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
+    if (kt + 1 < nk) {  // buffer cur^1 was last read in iteration kt-1 (barrier passed)
+      la.store(smem[cur ^ 1][0]);
+      lb.store(smem[cur ^ 1][1]);
+      if (kt + 2 < nk) {
+        la.load(A, lda, m0, M, kbeg + (int64_t)(kt + 2) * BK, kend);
+        lb.load(B, ldb, n0, N, kbeg + (int64_t)(kt + 2) * BK, kend);
+      }
+    }
+    const __bf16* As = smem[cur][0];
+    const __bf16* Bs = smem[cur][1];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag<LA>(As, wm * 64 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = frag<LB>(Bs, wn * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  write_tile_lds<TC, SPLIT>(acc, reinterpret_cast<float*>(&smem[0][0][0]), epi, C, ldc, b0, b1, bz, m0, n0, M, N, sp,
+                            wm, wn, lane);
+}
+}  // namespace bf
+
+// ============================== f32 kernel ================================================
+namespace f32 {
+constexpr int BK = 16, PAD = 4, LDW = BK + PAD;
+
+template <int LAYOUT, bool VEC>
+struct Loader {
+  static constexpr int NV = 128 * BK / 4 / NT;  // float4 per thread (=2)
+  float4 reg[NV];
+
+  __device__ __forceinline__ void load(const float* __restrict__ base, int64_t ld, int64_t r0,
+                                       int64_t rmax, int64_t k0, int64_t kmax) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * NT;
+      float t[4];
+      if (LAYOUT == 0) {
+        const int row = v / (BK / 4), kv = (v % (BK / 4)) * 4;
+        const int64_t gr = r0 + row, gk = k0 + kv;
+        if (VEC) {
+          reg[i] = (gr < rmax && gk < kmax) ? *reinterpret_cast<const float4*>(base + gr * ld + gk) : float4{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[e] = (gr < rmax && gk + e < kmax) ? base[gr * ld + gk + e] : 0.f;
+      } else {
+        const int krow = v / 32, rv = (v % 32) * 4;
+        const int64_t gk = k0 + krow, gr = r0 + rv;
+        if (VEC) {
+          reg[i] = (gk < kmax && gr < rmax) ? *reinterpret_cast<const float4*>(base + gk * ld + gr) : float4{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t[e] = (gk < kmax && gr + e < rmax) ? base[gk * ld + gr + e] : 0.f;
+      }
+      reg[i] = float4{t[0], t[1], t[2], t[3]};
+    }
+  }
+
+  __device__ __forceinline__ void store(float* __restrict__ lds) const {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = threadIdx.x + i * NT;
+      if (LAYOUT == 0) {
+        const int row = v / (BK / 4), kv = (v % (BK / 4)) * 4;
+        *reinterpret_cast<float4*>(lds + row * LDW + kv) = reg[i];
+      } else {
+        const int krow = v / 32, rv = (v % 32) * 4;
+        lds[(rv + 0) * LDW + krow] = reg[i].x;
+        lds[(rv + 1) * LDW + krow] = reg[i].y;
+        lds[(rv + 2) * LDW + krow] = reg[i].z;
+        lds[(rv + 3) * LDW + krow] = reg[i].w;
+      }
+    }
+  }
+};
+
+template <typename TC, int LA, int LB, bool VA, bool VB, bool SPLIT>
+__global__ void __launch_bounds__(NT)
+gemm_f32_kernel(const float* __restrict__ A, int64_t lda, int64_t sa0, int64_t sa1,
+                const float* __restrict__ B, int64_t ldb, int64_t sb0, int64_t sb1,
+                TC* __restrict__ C, int64_t ldc, int64_t sc0, int64_t sc1,
+                int64_t M, int64_t N, int64_t K, int64_t nb1, int tiles_n, Epi epi, Split sp) {
+  __shared__ __attribute__((aligned(16))) float smem[2][2][128 * LDW];
+
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int64_t bz = blockIdx.y, b0 = bz / nb1, b1 = bz % nb1;
+  A += b0 * sa0 + b1 * sa1;
+  B += b0 * sb0 + b1 * sb1;
+  C += b0 * sc0 + b1 * sc1;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  int64_t kbeg = 0, kend = K;
+  if (SPLIT) {
+    kbeg = (int64_t)blockIdx.z * sp.kchunk;
+    kend = kbeg + sp.kchunk < K ? kbeg + sp.kchunk : K;
+  }
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Loader<LA, VA> la;
+  Loader<LB, VB> lb;
+  const int nk = (int)((kend - kbeg + BK - 1) / BK);
+
+  if (nk > 0) {
+    la.load(A, lda, m0, M, kbeg, kend);
+    lb.load(B, ldb, n0, N, kbeg, kend);
+    la.store(smem[0][0]);
+    lb.store(smem[0][1]);
+  }
+  __syncthreads();
+
+  const int r = lane & 15, kq = (lane >> 4) * 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      la.load(A, lda, m0, M, (int64_t)(kt + 1) * BK, K);
-      lb.load(B, ldb, n0, N, (int64_t)(kt + 1) * BK, K);
+      la.load(A, lda, m0, M, kbeg + (int64_t)(kt + 1) * BK, kend);
+      lb.load(B, ldb, n0, N, kbeg + (int64_t)(kt + 1) * BK, kend);
     }
-    mma_tile<T>(smem[cur][0], smem[cur][1], acc, wm, wn, lane);
+    f32x4 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a[i] = *reinterpret_cast<const f32x4*>(smem[cur][0] + (wm * 64 + i * 16 + r) * LDW + kq);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      b[j] = *reinterpret_cast<const f32x4*>(smem[cur][1] + (wn * 64 + j * 16 + r) * LDW + kq);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
     if (more) {
       la.store(smem[cur ^ 1][0]);
       lb.store(smem[cur ^ 1][1]);
     }
     __syncthreads();
   }
+  write_tile<TC, SPLIT>(acc, epi, C, ldc, b0, b1, bz, m0, n0, M, N, sp, wm, wn, lane);
+}
+}  // namespace f32
 
-  // ---- epilogue: C layout col = lane&15, row = 4*(lane>>4)+r ----
-  const TC* R = epi.resid ? reinterpret_cast<const TC*>(epi.resid) + b0 * epi.sr0 + b1 * epi.sr1 : nullptr;
-  TC* X = epi.aux ? reinterpret_cast<TC*>(epi.aux) + b0 * epi.sx0 + b1 * epi.sx1 : nullptr;
-  const float* bias = epi.bias ? epi.bias + b0 * epi.sb0 + b1 * epi.sb1 : nullptr;
-  const int cl = lane & 15, rq = (lane >> 4) * 4;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t col = n0 + wn * 64 + j * 16 + cl;
-    if (col >= N) continue;
-    const float bcol = (bias && epi.bias_mode == 1) ? bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm * 64 + i * 16 + rq + r;
-        if (row >= M) continue;
-        float v = epi.alpha * acc[i][j][r] + bcol;
-        if (bias && epi.bias_mode == 2) v += bias[row];
-        if (X) X[row * epi.ldaux + col] = from_f32<TC>(v);
-        v = apply_act(epi.act, v);
-        if (R) v += epi.beta * to_f32(R[row * epi.ldr + col]);
-        C[row * ldc + col] = from_f32<TC>(v);
+// Sum the split-K partials in split order and apply the epilogue. One thread per 4 columns.
+template <typename TC>
+__global__ void __launch_bounds__(256)
+splitk_reduce_kernel(const float* __restrict__ ws, int splits, int64_t nb, int64_t nb1,
+                     TC* __restrict__ C, int64_t ldc, int64_t sc0, int64_t sc1,
+                     int64_t M, int64_t N, Epi epi) {
+  const int64_t n4 = (N + 3) / 4;
+  const int64_t total = nb * M * n4;
+  const int64_t plane = nb * M * N;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c4 = t % n4, rowg = t / n4;
+    const int64_t row = rowg % M, bz = rowg / M;
+    const int64_t b0 = bz / nb1, b1 = bz % nb1;
+    const int64_t col0 = c4 * 4;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* p = ws + bz * M * N + row * N + col0;
+    if (N % 4 == 0) {
+      for (int z = 0; z < splits; ++z) {
+        const float4 v = *reinterpret_cast<const float4*>(p + z * plane);
+        s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
       }
+    } else {
+      for (int z = 0; z < splits; ++z)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (col0 + e < N) s[e] += p[z * plane + e];
     }
+    TC* Cb = C + b0 * sc0 + b1 * sc1;
+    const TC* R = epi.resid ? reinterpret_cast<const TC*>(epi.resid) + b0 * epi.sr0 + b1 * epi.sr1 : nullptr;
+    TC* X = epi.aux ? reinterpret_cast<TC*>(epi.aux) + b0 * epi.sx0 + b1 * epi.sx1 : nullptr;
+    const float* bias = epi.bias ? epi.bias + b0 * epi.sb0 + b1 * epi.sb1 : nullptr;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (col0 + e < N) epi_store<TC>(epi, Cb, ldc, R, X, bias, row, col0 + e, s[e]);
   }
+}
+
+// ---- host side --------------------------------------------------------------------------
+constexpr int kCUs = 256;
+
+// Number of K splits: only when the output tiles cannot fill the chip and each split still
+// runs >= 8 k-tiles (splits * tiles ~ 2 waves of workgroups over the CUs).
+int choose_splits(const comet_gemm_args& a) {
+  if (a.split_k >= 1) return a.split_k;
+  const int64_t tiles = cdiv(a.m, BM) * cdiv(a.n, BN) * a.batch[0] * a.batch[1];
+  const int bk = a.dtype_ab == COMET_BF16 ? bf::BK : f32::BK;
+  const int64_t ktiles = cdiv(a.k, bk);
+  if (tiles >= kCUs || ktiles < 16) return 1;
+  int64_t s = cdiv(2 * kCUs, tiles);
+  const int64_t smax = ktiles / 8;
+  if (s > smax) s = smax;
+  if (s > 64) s = 64;
+  return s < 1 ? 1 : (int)s;
+}
+
+int64_t workspace_bytes(const comet_gemm_args& a, int splits) {
+  if (splits <= 1) return 0;
+  return (int64_t)splits * a.batch[0] * a.batch[1] * a.m * a.n * (int64_t)sizeof(float);
 }
 
 template <typename T, typename TC, int LA, int LB, bool VA, bool VB>
@@ -232,22 +601,61 @@ int launch(const comet_gemm_args& a, hipStream_t s) {
   const int64_t nb = a.batch[0] * a.batch[1];
   COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "comet_gemm: too many tiles");
   COMET_CHECK_ARG(nb <= 65535, "comet_gemm: batch too large (max 65535)");
+  auto v8 = [](const void* p, int64_t ld, const int64_t* st) {
+    return p == nullptr || ((uintptr_t)p % 32 == 0 && ld % 8 == 0 && st[0] % 8 == 0 && st[1] % 8 == 0);
+  };
+  const int vec = a.n % 8 == 0 && v8(a.c, a.ldc, a.stride_c) && v8(a.resid, a.ldr, a.stride_r) &&
+                  v8(a.aux, a.ldaux, a.stride_aux);
   Epi e{a.bias, a.bias_mode, a.stride_bias[0], a.stride_bias[1],
         a.resid, a.ldr, a.stride_r[0], a.stride_r[1], a.beta,
-        a.aux, a.ldaux, a.stride_aux[0], a.stride_aux[1], a.alpha, a.act};
-  dim3 grid((unsigned)(tiles_m * tiles_n), (unsigned)nb);
-  hipLaunchKernelGGL((gemm_kernel<T, TC, LA, LB, VA, VB>), grid, dim3(NT), 0, s,
-                     reinterpret_cast<const T*>(a.a), a.lda, a.stride_a[0], a.stride_a[1],
-                     reinterpret_cast<const T*>(a.b), a.ldb, a.stride_b[0], a.stride_b[1],
-                     reinterpret_cast<TC*>(a.c), a.ldc, a.stride_c[0], a.stride_c[1],
-                     a.m, a.n, a.k, a.batch[1], (int)tiles_n, e);
+        a.aux, a.ldaux, a.stride_aux[0], a.stride_aux[1], a.alpha, a.act, vec};
+  int splits = choose_splits(a);
+  const int bk = std::is_same<T, __bf16>::value ? bf::BK : f32::BK;
+  if (splits > 1 && (a.workspace == nullptr || a.workspace_bytes < workspace_bytes(a, splits))) splits = 1;
+  int64_t kchunk = a.k;
+  if (splits > 1) {
+    kchunk = cdiv(cdiv(a.k, bk), splits) * bk;
+    splits = (int)cdiv(a.k, kchunk);
+  }
+  Split sp{reinterpret_cast<float*>(a.workspace), kchunk};
+  dim3 grid((unsigned)(tiles_m * tiles_n), (unsigned)nb, (unsigned)splits);
+  const T* A = reinterpret_cast<const T*>(a.a);
+  const T* B = reinterpret_cast<const T*>(a.b);
+  TC* C = reinterpret_cast<TC*>(a.c);
+  if constexpr (std::is_same<T, __bf16>::value) {
+    if (splits > 1)
+      hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, LA, LB, VA, VB, true>), grid, dim3(NT), 0, s,
+                         A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
+                         C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1], (int)tiles_n, e, sp);
+    else
+      hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, LA, LB, VA, VB, false>), grid, dim3(NT), 0, s,
+                         A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
+                         C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1], (int)tiles_n, e, sp);
+  } else {
+    if (splits > 1)
+      hipLaunchKernelGGL((f32::gemm_f32_kernel<TC, LA, LB, VA, VB, true>), grid, dim3(NT), 0, s,
+                         A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
+                         C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1], (int)tiles_n, e, sp);
+    else
+      hipLaunchKernelGGL((f32::gemm_f32_kernel<TC, LA, LB, VA, VB, false>), grid, dim3(NT), 0, s,
+                         A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
+                         C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1], (int)tiles_n, e, sp);
+  }
   COMET_CHECK_LAUNCH("comet_gemm");
+  if (splits > 1) {
+    const int64_t work = nb * a.m * cdiv(a.n, 4);
+    int64_t blocks = cdiv(work, 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL((splitk_reduce_kernel<TC>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       sp.ws, splits, nb, a.batch[1], C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, e);
+    COMET_CHECK_LAUNCH("comet_gemm split-K reduce");
+  }
   return COMET_OK;
 }
 
 template <typename T, typename TC, int LA, int LB>
 int dispatch_vec(const comet_gemm_args& a, hipStream_t s) {
-  constexpr int V = Cfg<T>::VEC;
+  constexpr int V = 16 / sizeof(T);
   // A vector needs 16-byte alignment of every vector start: base, ld and strides multiples of V.
   auto aligned = [&](const void* p, int64_t ld, const int64_t* st, int64_t contig_extent) {
     return ((uintptr_t)p % 16 == 0) && ld % V == 0 && st[0] % V == 0 && st[1] % V == 0 &&
@@ -269,12 +677,7 @@ int dispatch_layout(const comet_gemm_args& a, hipStream_t s) {
   return dispatch_vec<T, TC, 1, 1>(a, s);
 }
 
-}  // namespace
-
-}  // namespace comet
-
-extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
-  using namespace comet;
+int validate(const comet_gemm_args* args) {
   COMET_CHECK_ARG(args != nullptr, "comet_gemm: null args");
   const comet_gemm_args& a = *args;
   COMET_CHECK_ARG(a.m >= 0 && a.n >= 0 && a.k >= 0, "comet_gemm: negative dims");
@@ -282,6 +685,69 @@ extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   COMET_CHECK_ARG(a.layout_b == 0 || a.layout_b == 1, "comet_gemm: bad layout_b");
   COMET_CHECK_ARG(a.batch[0] >= 1 && a.batch[1] >= 1, "comet_gemm: batch dims must be >= 1");
   COMET_CHECK_ARG(a.bias_mode >= 0 && a.bias_mode <= 2, "comet_gemm: bad bias_mode");
+  COMET_CHECK_ARG(a.split_k >= 0 && a.split_k <= 256, "comet_gemm: split_k must be in [0, 256]");
+  COMET_CHECK_ARG(a.workspace_bytes >= 0, "comet_gemm: negative workspace_bytes");
+  return COMET_OK;
+}
+
+template <typename TC>
+int launch_conv(const comet_conv_args& a, hipStream_t s) {
+  const int64_t oh = (a.h + 2 * a.pad - a.kh) / a.stride + 1, ow = (a.w + 2 * a.pad - a.kw) / a.stride + 1;
+  const int64_t M = a.n * oh * ow, N = a.cout, K = (int64_t)a.kh * a.kw * a.c;
+  const int64_t tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
+  COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "comet_conv2d_nhwc: too many tiles");
+  const int vec = a.cout % 8 == 0 && (uintptr_t)a.y % 32 == 0 && a.ldy % 8 == 0 &&
+                  (a.resid == nullptr || ((uintptr_t)a.resid % 32 == 0 && a.ldr % 8 == 0));
+  Epi e{a.bias, a.bias ? 1 : 0, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, 1.f, a.act, vec};
+  bf::ConvGeo g{reinterpret_cast<const __bf16*>(a.x), (int)a.h, (int)a.w, (int)a.c, a.kw, a.stride, a.pad,
+                (int)oh, (int)ow};
+  Split sp{nullptr, K};
+  hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, 0, 0, true, true, false, true>),
+                     dim3((unsigned)(tiles_m * tiles_n), 1, 1), dim3(NT), 0, s,
+                     nullptr, 0, 0, 0, reinterpret_cast<const __bf16*>(a.weight), a.ldw, 0, 0,
+                     reinterpret_cast<TC*>(a.y), a.ldy, 0, 0, M, N, K, 1, (int)tiles_n, e, sp, g);
+  COMET_CHECK_LAUNCH("comet_conv2d_nhwc");
+  return COMET_OK;
+}
+
+}  // namespace
+
+}  // namespace comet
+
+extern "C" int comet_conv2d_nhwc(const comet_conv_args* args, void* stream) {
+  using namespace comet;
+  COMET_CHECK_ARG(args != nullptr, "comet_conv2d_nhwc: null args");
+  const comet_conv_args& a = *args;
+  COMET_CHECK_ARG(a.dtype == COMET_BF16, "comet_conv2d_nhwc: x/weight must be bf16 (use im2col + comet_gemm for f32)");
+  COMET_CHECK_ARG(a.c > 0 && a.c % 8 == 0, "comet_conv2d_nhwc: channels must be a positive multiple of 8");
+  COMET_CHECK_ARG(a.n > 0 && a.h > 0 && a.w > 0 && a.cout > 0 && a.kh > 0 && a.kw > 0 && a.stride > 0 && a.pad >= 0,
+                  "comet_conv2d_nhwc: bad geometry");
+  COMET_CHECK_ARG(a.h + 2 * a.pad >= a.kh && a.w + 2 * a.pad >= a.kw, "comet_conv2d_nhwc: kernel larger than padded input");
+  COMET_CHECK_ARG(a.ldw >= (int64_t)a.kh * a.kw * a.c && a.ldw % 8 == 0, "comet_conv2d_nhwc: ldw < kh*kw*c or not a multiple of 8");
+  COMET_CHECK_ARG(a.x && a.weight && a.y, "comet_conv2d_nhwc: null pointer");
+  COMET_CHECK_ARG((uintptr_t)a.x % 16 == 0 && (uintptr_t)a.weight % 16 == 0, "comet_conv2d_nhwc: x/weight must be 16-byte aligned");
+  COMET_CHECK_ARG(a.n * a.h * a.w * a.c < (1ll << 40), "comet_conv2d_nhwc: input too large");
+  hipStream_t s = as_stream(stream);
+  if (a.dtype_y == COMET_BF16) return launch_conv<__bf16>(a, s);
+  if (a.dtype_y == COMET_F32) return launch_conv<float>(a, s);
+  set_error("comet_conv2d_nhwc: bad dtype_y");
+  return COMET_EINVAL;
+}
+
+extern "C" int comet_gemm_workspace(const comet_gemm_args* args, int64_t* bytes) {
+  using namespace comet;
+  const int rc = validate(args);
+  if (rc != COMET_OK) return rc;
+  COMET_CHECK_ARG(bytes != nullptr, "comet_gemm_workspace: null bytes");
+  *bytes = workspace_bytes(*args, choose_splits(*args));
+  return COMET_OK;
+}
+
+extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
+  using namespace comet;
+  const int rc = validate(args);
+  if (rc != COMET_OK) return rc;
+  const comet_gemm_args& a = *args;
   COMET_CHECK_ARG(a.a && a.b && a.c, "comet_gemm: null operand");
   if (a.m == 0 || a.n == 0) return COMET_OK;
   hipStream_t s = as_stream(stream);

@@ -7,6 +7,10 @@
 // minipytorch3d/rotation_conversions.py:382-449 (quaternion ops).
 #include "common.hpp"
 
+// The reference evaluates these formulas as separate f32 tensor ops: keep every product and sum
+// rounded on its own (no FMA contraction) so the tiny head kernels match it to the ulp.
+#pragma clang fp contract(off)
+
 namespace comet {
 namespace {
 
@@ -98,7 +102,7 @@ __global__ void harmonic_fwd_kernel(const float* __restrict__ x, const float* __
     } else {
       const int p = (int)(c / ((int64_t)dim * n));
       const int i = (int)((c / n) % dim), k = (int)(c % n);
-      const float e = x[r * dim + i] * freqs[k] + (p ? half_pi : 0.f);  // f32 argument, as the reference
+      const float e = x[r * dim + i] * freqs[k] + (p ? half_pi : 0.f);  // f32, as the reference
       v = (float)sin((double)e);  // correctly rounded: large |x*f| would lose accuracy in sinf
       if (cov) v *= expf(-0.5f * (cov[r * dim + i] * (freqs[k] * freqs[k])));
     }

@@ -168,6 +168,149 @@ instnorm_nhwc_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __re
   }
 }
 
+// ---- InstanceNorm, vectorised (c % 8 == 0) ------------------------------------------------
+// Each thread owns 8 channels of one pixel slot; a block covers `chunk` pixels of one image.
+// Statistics are shifted sums (shift = the image's first pixel, per channel) so the variance is
+// taken about a value near the mean: s1 = sum(x - K), s2 = sum((x - K)^2). Large images split
+// over chunks: in_stats_kernel writes per-chunk partials, in_apply_kernel (or the fused kernel for
+// a single chunk) combines them and normalises.
+struct INGeo { int64_t hw, chunk; int c, chunks; float eps; int relu, relu_inner; };
+
+template <typename T>
+__device__ __forceinline__ void in_block_stats(const T* __restrict__ xb, const INGeo& g, int64_t p0,
+                                               int64_t p1, float* __restrict__ red, float* out1,
+                                               float* out2) {
+  const int tpp = g.c / 8, ppp = 256 / tpp;
+  const int t = threadIdx.x, cg = t % tpp, slot = t / tpp;
+  float s1[8], s2[8], K[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  if (slot < ppp) {
+    load8(xb + cg * 8, K);
+    for (int64_t p = p0 + slot; p < p1; p += ppp) {
+      float v[8];
+      load8(xb + p * g.c + cg * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[e] - K[e];
+        s1[e] += d;
+        s2[e] += d * d;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[slot * g.c + cg * 8 + e] = s1[e];
+      red[2048 + slot * g.c + cg * 8 + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  for (int ch = t; ch < g.c; ch += 256) {
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < ppp; ++q) {
+      a += red[q * g.c + ch];
+      b += red[2048 + q * g.c + ch];
+    }
+    out1[ch] = a;
+    out2[ch] = b;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void in_block_apply(const T* __restrict__ xb, const T* __restrict__ rb,
+                                               T* __restrict__ yb, const INGeo& g, int64_t p0, int64_t p1,
+                                               const float* mean, const float* rstd) {
+  const int tpp = g.c / 8, ppp = 256 / tpp;
+  const int t = threadIdx.x, cg = t % tpp, slot = t / tpp;
+  if (slot >= ppp) return;
+  float mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    mu[e] = mean[cg * 8 + e];
+    rs[e] = rstd[cg * 8 + e];
+  }
+  for (int64_t p = p0 + slot; p < p1; p += ppp) {
+    float v[8];
+    load8(xb + p * g.c + cg * 8, v);
+    float r[8];
+    if (rb) load8(rb + p * g.c + cg * 8, r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float o = (v[e] - mu[e]) * rs[e];
+      if (g.relu_inner) o = o > 0.f ? o : 0.f;
+      if (rb) o += r[e];
+      if (g.relu) o = o > 0.f ? o : 0.f;
+      v[e] = o;
+    }
+    store8(yb + p * g.c + cg * 8, v);
+  }
+}
+
+// mean / rstd of image n from its first-pixel shift K and the summed shifted moments
+template <typename T>
+__device__ __forceinline__ void in_finish(const T* __restrict__ xb, const INGeo& g, int ch, float S1,
+                                          float S2, float* mean, float* rstd) {
+  const float inv = 1.f / (float)g.hw;
+  const float m1 = S1 * inv;
+  float var = S2 * inv - m1 * m1;
+  var = var > 0.f ? var : 0.f;
+  mean[ch] = to_f32(xb[ch]) + m1;
+  rstd[ch] = rsqrtf(var + g.eps);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+in_fused_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y, INGeo g) {
+  __shared__ float red[4096];
+  __shared__ float st[4][256];
+  const int64_t n = blockIdx.x;
+  const T* xb = x + n * g.hw * g.c;
+  in_block_stats(xb, g, 0, g.hw, red, st[0], st[1]);
+  __syncthreads();
+  for (int ch = threadIdx.x; ch < g.c; ch += 256) in_finish(xb, g, ch, st[0][ch], st[1][ch], st[2], st[3]);
+  __syncthreads();
+  in_block_apply(xb, res ? res + n * g.hw * g.c : nullptr, y + n * g.hw * g.c, g, 0, g.hw, st[2], st[3]);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+in_stats_kernel(const T* __restrict__ x, float* __restrict__ part, INGeo g) {
+  __shared__ float red[4096];
+  const int64_t n = blockIdx.y, k = blockIdx.x;
+  const int64_t p0 = k * g.chunk, p1 = p0 + g.chunk < g.hw ? p0 + g.chunk : g.hw;
+  float* out = part + (n * g.chunks + k) * 2 * g.c;
+  in_block_stats(x + n * g.hw * g.c, g, p0, p1, red, out, out + g.c);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+in_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restrict__ y,
+                const float* __restrict__ part, INGeo g) {
+  __shared__ float st[2][256];
+  const int64_t n = blockIdx.y, k = blockIdx.x;
+  const T* xb = x + n * g.hw * g.c;
+  for (int ch = threadIdx.x; ch < g.c; ch += 256) {
+    float S1 = 0.f, S2 = 0.f;
+    const float* pp = part + n * g.chunks * 2 * g.c;
+    for (int q = 0; q < g.chunks; ++q) {
+      S1 += pp[q * 2 * g.c + ch];
+      S2 += pp[q * 2 * g.c + g.c + ch];
+    }
+    in_finish(xb, g, ch, S1, S2, st[0], st[1]);
+  }
+  __syncthreads();
+  const int64_t p0 = k * g.chunk, p1 = p0 + g.chunk < g.hw ? p0 + g.chunk : g.hw;
+  in_block_apply(xb, res ? res + n * g.hw * g.c : nullptr, y + n * g.hw * g.c, g, p0, p1, st[0], st[1]);
+}
+
+// chunks per image: ~1024 blocks over the launch, >= 4 pixel passes per block
+inline int in_chunks(int64_t n, int64_t hw, int64_t c) {
+  const int64_t ppp = 256 / (c / 8);
+  int64_t want = cdiv(1024, n);
+  const int64_t most = hw / (ppp * 4);
+  if (want > most) want = most;
+  return (int)(want < 1 ? 1 : want);
+}
+
 }  // namespace
 }  // namespace comet
 
@@ -217,10 +360,45 @@ extern "C" int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, con
   return COMET_OK;
 }
 
+extern "C" int comet_instnorm_workspace(int64_t n, int64_t hw, int64_t c, int64_t* bytes) {
+  COMET_CHECK_ARG(bytes && n > 0 && hw > 0 && c > 0, "comet_instnorm_workspace: bad args");
+  *bytes = 0;
+  if (c % 8 == 0 && c <= 256) {
+    const int chunks = in_chunks(n, hw, c);
+    if (chunks > 1) *bytes = n * chunks * 2 * c * (int64_t)sizeof(float);
+  }
+  return COMET_OK;
+}
+
 extern "C" int comet_instnorm_nhwc(int dtype, const void* x, const void* res, void* y, int64_t n,
                                    int64_t hw, int64_t c, float eps, int relu, int res_norm_relu,
-                                   void* stream) {
+                                   void* workspace, int64_t workspace_bytes, void* stream) {
   COMET_CHECK_ARG(x && y && n > 0 && hw > 0 && c > 0, "comet_instnorm_nhwc: bad args");
+  const bool aligned = ((uintptr_t)x | (uintptr_t)y | (uintptr_t)res) % 32 == 0;
+  if (c % 8 == 0 && c <= 256 && aligned && n <= 65535ll * 65535ll) {
+    hipStream_t s = as_stream(stream);
+    int chunks = in_chunks(n, hw, c);
+    if (chunks > 1 && (!workspace || workspace_bytes < n * chunks * 2 * c * (int64_t)sizeof(float))) chunks = 1;
+    INGeo g{hw, cdiv(hw, chunks), (int)c, chunks, eps, relu, res_norm_relu};
+#define INL(T)                                                                                           \
+  if (chunks == 1) {                                                                                     \
+    COMET_CHECK_ARG(n <= 2147483647ll, "comet_instnorm_nhwc: too many images");                         \
+    hipLaunchKernelGGL((in_fused_kernel<T>), dim3((unsigned)n), dim3(256), 0, s, (const T*)x,            \
+                       (const T*)res, (T*)y, g);                                                         \
+  } else {                                                                                               \
+    COMET_CHECK_ARG(n <= 65535, "comet_instnorm_nhwc: too many images for the chunked path");          \
+    hipLaunchKernelGGL((in_stats_kernel<T>), dim3((unsigned)chunks, (unsigned)n), dim3(256), 0, s,       \
+                       (const T*)x, (float*)workspace, g);                                               \
+    hipLaunchKernelGGL((in_apply_kernel<T>), dim3((unsigned)chunks, (unsigned)n), dim3(256), 0, s,       \
+                       (const T*)x, (const T*)res, (T*)y, (const float*)workspace, g);                   \
+  }
+    if (dtype == COMET_F32) { INL(float) }
+    else if (dtype == COMET_BF16) { INL(__bf16) }
+    else { set_error("comet_instnorm_nhwc: bad dtype"); return COMET_EINVAL; }
+#undef INL
+    COMET_CHECK_LAUNCH("comet_instnorm_nhwc");
+    return COMET_OK;
+  }
   COMET_CHECK_ARG(cdiv(c, 64) <= 65535, "comet_instnorm_nhwc: c too large");
   dim3 grid((unsigned)n, (unsigned)cdiv(c, 64));
   hipStream_t s = as_stream(stream);

@@ -54,6 +54,11 @@ const char* comet_last_error(void);
  * layout_a 0: A[m*lda + k]; 1: A[k*lda + m].  layout_b 0: B[n*ldb + k] (Linear weight
  * [out,in]); 1: B[k*ldb + n]. Two batch dimensions: element base = b0*stride[0] + b1*stride[1].
  * Bias is always f32; c / resid / aux use dtype_c.
+ *
+ * Split-K: split_k 0 = library heuristic (splits K when the output tiles cannot fill the 256 CUs,
+ * e.g. weight gradients reduced over every token), 1 = never, s > 1 = force s splits. A split
+ * GEMM needs an f32 workspace of comet_gemm_workspace() bytes; with workspace == NULL (or too
+ * small) the GEMM runs unsplit. Partials are summed in a fixed order: results are deterministic.
  * ------------------------------------------------------------------------------------- */
 typedef struct comet_gemm_args {
   int32_t dtype_ab;
@@ -70,9 +75,36 @@ typedef struct comet_gemm_args {
   void* aux; int64_t ldaux; int64_t stride_aux[2];
   float alpha; float beta;
   int32_t act;
+  void* workspace; int64_t workspace_bytes;
+  int32_t split_k;
 } comet_gemm_args;
 
 int comet_gemm(const comet_gemm_args* args, void* stream);
+/* Workspace bytes comet_gemm needs for these arguments (0 when it will not split K). */
+int comet_gemm_workspace(const comet_gemm_args* args, int64_t* bytes);
+
+/* ---------------------------------------------------------------------------------------
+ * Implicit-GEMM convolution on channels-last activations (nn.Conv2d of BasicEncoder /
+ * ShallowEncoder / ResidualBlock, blocks.py:27-202, modules.py:39-116): the im2col matrix is
+ * never materialised; the GEMM's A tiles are gathered from x directly.
+ *   y[(n*oh + oy)*ow + ox][co] = act(bias[co] + sum_{ky,kx,ci} x[n][oy*s-p+ky][ox*s-p+kx][ci]
+ *                                    * weight[co][(ky*kw + kx)*c + ci]) + beta*resid[...]
+ * x [n,h,w,c] bf16 contiguous with c % 8 == 0; weight [cout][ldw] bf16 (K = kh*kw*c <= ldw);
+ * y / resid use dtype_y with row pitch ldy / ldr. (f32 or c % 8 != 0: im2col + comet_gemm.)
+ * ------------------------------------------------------------------------------------- */
+typedef struct comet_conv_args {
+  int32_t dtype;      /* x and weight: COMET_BF16 */
+  int32_t dtype_y;
+  const void* x; int64_t n, h, w, c;
+  const void* weight; int64_t cout, ldw;
+  int32_t kh, kw, stride, pad;
+  const float* bias;
+  void* y; int64_t ldy;
+  const void* resid; int64_t ldr; float beta;
+  int32_t act;
+} comet_conv_args;
+
+int comet_conv2d_nhwc(const comet_conv_args* args, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Row LayerNorm over the last dim (nn.LayerNorm; also GroupNorm(1, C) on [rows, C] as used
@@ -159,10 +191,13 @@ int comet_im2col_nhwc(int dtype_in, int dtype_out, const void* x, void* cols, in
                       int64_t oh, int64_t ow, int64_t ldc, void* stream);
 /* InstanceNorm2d (affine=False, eps 1e-5) on NHWC, optional residual add and ReLU:
  * o = IN(x); if res_norm_relu: o = relu(o); if res: o += res; if relu: o = relu(o).
- * (ResidualBlock tail relu(x + relu(IN(conv2(.)))), modules.py:108-116). */
+ * (ResidualBlock tail relu(x + relu(IN(conv2(.)))), modules.py:108-116).
+ * Large images are split over several workgroups per image; that path needs an f32 workspace
+ * of comet_instnorm_workspace() bytes (with a NULL / short workspace one workgroup per image). */
+int comet_instnorm_workspace(int64_t n, int64_t hw, int64_t c, int64_t* bytes);
 int comet_instnorm_nhwc(int dtype, const void* x, const void* res, void* y, int64_t n,
                         int64_t hw, int64_t c, float eps, int relu, int res_norm_relu,
-                        void* stream);
+                        void* workspace, int64_t workspace_bytes, void* stream);
 /* bilinear resize, align_corners=True, NCHW or NHWC (F.interpolate, blocks.py:179-202,
  * track_predictor.py:137, camera_predictor10.py:624). add != 0 accumulates into y. */
 int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, const void* x, void* y,

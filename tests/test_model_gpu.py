@@ -183,8 +183,10 @@ def test_harmonic_embedding_against_reference(gold):
     cc = cov.clone().requires_grad_(True)
     m = HarmonicEmbedding(10, 0.5, False, True).cuda()
     m(xx, diag_cov=cc).backward(g.float().cuda())
-    close(xx.grad, xr.grad, 1e-4, 1e-4, "harmonic dx")
-    close(cc.grad, cr.grad, 1e-4, 1e-4, "harmonic dcov")
+    # f32 evaluation (the reference's own dtype) vs f64: f^2 up to 6.6e4 amplifies the argument's f32
+    # rounding, so the reference itself is 5e-5 x max|grad| away from f64; tolerance scales with max
+    close(xx.grad, xr.grad, 1e-4, 1e-4 * xr.grad.abs().max().item(), "harmonic dx")
+    close(cc.grad, cr.grad, 1e-4, 2e-4 * cr.grad.abs().max().item(), "harmonic dcov")
 
 
 def test_train_step_matches_oracle_adamw(setup):

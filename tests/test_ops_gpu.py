@@ -49,6 +49,79 @@ def test_gemm_layouts(dtype, la, lb, mnk):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("mnk,split", [((128, 128, 8192), 0), ((200, 136, 5000), 0), ((130, 77, 4099), 0),
+                                       ((96, 40, 3001), 7), ((256, 384, 2048), 3)])
+def test_gemm_splitk(dtype, la, lb, mnk, split):
+    """Split-K path (weight-gradient shapes: few output tiles, long K), auto and forced splits,
+    vectorised and scalar (misaligned) loaders; partial sums reduced in a fixed order."""
+    ops = _ops()
+    M, N, K = mnk
+    A = _rand(M, K, dtype=dtype, seed=11)
+    B = _rand(N, K, dtype=dtype, seed=12)
+    ref = A.double() @ B.double().t()
+    Ad = (A if la == 0 else A.t().contiguous()).to(DEV)
+    Bd = (B if lb == 0 else B.t().contiguous()).to(DEV)
+    outs = []
+    for _ in range(2):
+        C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+        ops.gemm_raw(Ad, Bd, C, m=M, n=N, k=K, layout_a=la, lda=(K if la == 0 else M),
+                     layout_b=lb, ldb=(K if lb == 0 else N), ldc=N, split_k=split)
+        outs.append(C)
+    tol = 2e-5 if dtype == torch.float32 else 1e-3
+    _close(outs[0], ref, tol, tol * math.sqrt(K), f"splitk gemm {dtype} la={la} lb={lb} {mnk} split={split}")
+    assert torch.equal(outs[0], outs[1]), "split-K result not deterministic"
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_splitk_epilogue_batched(dtype):
+    ops = _ops()
+    nb0, nb1, M, N, K = 2, 3, 72, 136, 1536
+    A = _rand(nb0, nb1, K, M, dtype=dtype, seed=13)           # layout 1 (dW-like: A[k*lda + m])
+    B = _rand(nb0, nb1, K, N, dtype=dtype, seed=14)           # layout 1
+    bias = _rand(nb0, nb1, M, seed=15)                        # per-row bias
+    r = _rand(nb0, nb1, M, N, seed=16)
+    pre = torch.einsum("abkm,abkn->abmn", A.double(), B.double()) * 0.5 + bias.double()[..., None]
+    ref = F.relu(pre) + 2.0 * r.double()
+    out = torch.empty(nb0, nb1, M, N, device=DEV, dtype=torch.float32)
+    aux = torch.empty_like(out)
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    ops.gemm_raw(Ad, Bd, out, m=M, n=N, k=K, layout_a=1, lda=M, layout_b=1, ldb=N, ldc=N, batch=(nb0, nb1),
+                 stride_a=(nb1 * K * M, K * M), stride_b=(nb1 * K * N, K * N), stride_c=(nb1 * M * N, M * N),
+                 bias=bias.to(DEV), bias_mode=2, stride_bias=(nb1 * M, M), resid=r.to(DEV), ldr=N,
+                 stride_r=(nb1 * M * N, M * N), beta=2.0, aux=aux, ldaux=N, stride_aux=(nb1 * M * N, M * N),
+                 alpha=0.5, act=2, split_k=4)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    _close(out, ref, tol, 1e-3 * math.sqrt(K) / 10, "split epilogue out")
+    _close(aux, pre, tol, 1e-3 * math.sqrt(K) / 10, "split epilogue aux")
+
+
+@pytest.mark.parametrize("geo", [(3, 17, 13, 16, 40, 3, 1, 1), (2, 33, 30, 64, 96, 3, 2, 1), (2, 16, 16, 32, 32, 1, 2, 0),
+                                 (1, 12, 12, 416, 256, 3, 1, 1), (2, 20, 18, 8, 64, 7, 2, 3), (65, 9, 9, 32, 32, 3, 2, 1)])
+@pytest.mark.parametrize("epi", ["bias", "bias_relu_resid"])
+def test_conv2d_nhwc_implicit_gemm(geo, epi):
+    """comet_conv2d_nhwc (implicit GEMM, bf16) vs torch conv2d in f64 on the same bf16 inputs."""
+    ops = _ops()
+    n, h, w, c, cout, k, s, p = geo
+    x = _rand(n, c, h, w, seed=20).to(torch.bfloat16)
+    wt = _rand(cout, c, k, k, seed=21, scale=1.0 / math.sqrt(c * k * k)).to(torch.bfloat16)
+    b = _rand(cout, seed=22)
+    ref = F.conv2d(x.double(), wt.double(), b.double(), stride=s, padding=p).permute(0, 2, 3, 1)
+    K = c * k * k
+    Kp = (K + 7) // 8 * 8
+    wm = torch.zeros(cout, Kp, dtype=torch.bfloat16)
+    wm[:, :K] = wt.permute(0, 2, 3, 1).reshape(cout, K)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    kw = dict(bias=b.to(DEV), out_dtype=torch.float32)
+    if epi == "bias_relu_resid":
+        r = _rand(*ref.shape, seed=23)
+        ref = F.relu(ref) + 0.5 * r.double()
+        kw.update(act=2, resid=r.to(DEV), beta=0.5)
+    y = ops.conv2d_nhwc(xd, wm.to(DEV), k, k, s, p, **kw)
+    _close(y, ref, 1e-3, 1e-3, f"conv {geo} {epi}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_gemm_epilogue_bias_gelu_resid_aux(dtype):
     ops = _ops()
     M, N, K = 257, 384, 192
@@ -193,3 +266,35 @@ def test_instnorm_and_resize():
         _close(y1, r, 1e-5, 1e-5, f"resize nchw {oh}x{ow}")
         y2 = ops.resize_bilinear(x.permute(0, 2, 3, 1).contiguous().to(DEV), oh, ow, nhwc=True)
         _close(y2.permute(0, 3, 1, 2), r, 1e-5, 1e-5, f"resize nhwc {oh}x{ow}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,c,h,w", [(2, 96, 128, 128), (700, 32, 16, 16), (3, 12, 9, 7), (5, 256, 33, 17), (1, 64, 8, 8)])
+@pytest.mark.parametrize("mode", ["plain", "inner_res_relu"])
+def test_instnorm_shapes(dtype, n, c, h, w, mode):
+    """Chunked (partials + apply), fused (one block per image) and generic (c % 8 != 0) paths;
+    inputs with a large common offset exercise the shifted-moment variance."""
+    ops = _ops()
+    x = (_rand(n, c, h, w, seed=30) * 0.5 + 40.0).to(dtype)
+    res = _rand(n, c, h, w, seed=31).to(dtype) if mode != "plain" else None
+    ref = F.instance_norm(x.double(), eps=1e-5)
+    if mode != "plain":
+        ref = F.relu(F.relu(ref) + res.double())
+    y = ops.instnorm_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV),
+                          res.permute(0, 2, 3, 1).contiguous().to(DEV) if res is not None else None,
+                          relu=mode != "plain", relu_inner=mode != "plain")
+    tol = 2e-4 if dtype == torch.float32 else 1.6e-2
+    _close(y.permute(0, 3, 1, 2), ref, tol, tol, f"instnorm {dtype} {(n, c, h, w)} {mode}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_resize_nhwc_vector_add(dtype):
+    ops = _ops()
+    x = _rand(4, 64, 37, 29, seed=32).to(dtype)
+    base = _rand(4, 64, 64, 64, seed=33).to(dtype)
+    ref = F.interpolate(x.double(), (64, 64), mode="bilinear", align_corners=True) + base.double()
+    out = base.permute(0, 2, 3, 1).contiguous().to(DEV)
+    ops.resize_bilinear(x.permute(0, 2, 3, 1).contiguous().to(DEV), 64, 64, nhwc=True, out=out, add=True)
+    # f32 coordinates as ATen (align_corners lambdas in f32) vs an f64 reference
+    tol = 5e-5 if dtype == torch.float32 else 1.6e-2
+    _close(out.permute(0, 3, 1, 2), ref, tol, tol, f"resize nhwc add {dtype}")
