@@ -29,6 +29,7 @@ class GemmArgs(ctypes.Structure):
         ("aux", c_vp), ("ldaux", c_i64), ("stride_aux", c_i64 * 2),
         ("alpha", ctypes.c_float), ("beta", ctypes.c_float), ("act", c_i32),
         ("workspace", c_vp), ("workspace_bytes", c_i64), ("split_k", c_i32),
+        ("convert_a", c_i32), ("convert_b", c_i32),
     ]
 
 
@@ -57,6 +58,22 @@ class AttnArgs(ctypes.Structure):
     ]
 
 
+class AttnBwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", c_i32), ("head_dim", c_i32),
+        ("batch", c_i64), ("heads", c_i64), ("lq", c_i64), ("lk", c_i64),
+        ("q", c_vp), ("sq_b", c_i64), ("sq_h", c_i64), ("sq_l", c_i64),
+        ("k", c_vp), ("sk_b", c_i64), ("sk_h", c_i64), ("sk_l", c_i64),
+        ("v", c_vp), ("sv_b", c_i64), ("sv_h", c_i64), ("sv_l", c_i64),
+        ("o", c_vp), ("so_b", c_i64), ("so_h", c_i64), ("so_l", c_i64),
+        ("dout", c_vp), ("sd_b", c_i64), ("sd_h", c_i64), ("sd_l", c_i64),
+        ("dq", c_vp), ("sdq_b", c_i64), ("sdq_h", c_i64), ("sdq_l", c_i64),
+        ("dk", c_vp), ("sdk_b", c_i64), ("sdk_h", c_i64), ("sdk_l", c_i64),
+        ("dv", c_vp), ("sdv_b", c_i64), ("sdv_h", c_i64), ("sdv_l", c_i64),
+        ("lse", c_vp), ("delta", c_vp), ("scale", ctypes.c_float),
+    ]
+
+
 # (name, restype, argtypes); every exported symbol of include/comet_hip.h
 _F = ctypes.c_float
 _INT = ctypes.c_int
@@ -66,8 +83,11 @@ SIGNATURES = {
     "comet_gemm": (_INT, [ctypes.POINTER(GemmArgs), c_vp]),
     "comet_gemm_workspace": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64)]),
     "comet_conv2d_nhwc": (_INT, [ctypes.POINTER(ConvArgs), c_vp]),
-    "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _F, _INT, c_vp]),
-    "comet_layernorm_bwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, _INT, c_vp]),
+    "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
+                                   c_i64, _F, _INT, c_vp]),
+    "comet_layernorm_bwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, _INT, c_vp, c_vp, c_vp, c_i64, c_i64,
+                                   _INT, c_vp]),
+    "comet_attention_bwd": (_INT, [ctypes.POINTER(AttnBwdArgs), c_vp]),
     "comet_attention_fwd": (_INT, [ctypes.POINTER(AttnArgs), c_vp]),
     "comet_attn_probs": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _F, c_vp]),
     "comet_attn_delta": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
@@ -75,6 +95,7 @@ SIGNATURES = {
     "comet_cast": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_vp]),
     "comet_act_bwd": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_vp, _INT, c_i64, c_vp]),
     "comet_axpby": (_INT, [c_vp, c_vp, _F, _F, c_i64, c_vp]),
+    "comet_act_bwd_colsum": (_INT, [_INT, _INT, c_vp, _INT, c_vp, _INT, c_vp, c_vp, c_i64, c_i64, _INT, c_vp]),
     "comet_colsum": (_INT, [_INT, c_vp, c_vp, c_i64, c_i64, c_i64, _INT, c_vp]),
     "comet_sq_norm_multi": (_INT, [c_vp, c_vp, _INT, c_vp, c_vp]),
     "comet_adamw_multi": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, _INT, _F, _F, _F, _F, _F, _INT, c_vp, _F, c_vp]),

@@ -106,23 +106,43 @@ def to_compute(x):
 # ------------------------------------------------------------------------------------------
 # linear: y = act(x W^T + b) + beta * resid
 # ------------------------------------------------------------------------------------------
-def _linear_bwd(x2, wc, dpre, need_dx, need_dw, need_db, dx_dtype):
-    """dpre [M, N] (compute dtype or f32) -> dx [M, K] (dx_dtype), dW [N, K] f32, db [N] f32."""
-    M, N = dpre.shape
+def _vec8(t):
+    return t.is_contiguous() and t.shape[-1] % 8 == 0 and t.data_ptr() % 32 == 0
+
+
+def _linear_bwd(x2, wc, dy2, act, aux, need_dx, need_dw, need_db, dx_dtype):
+    """dy2 [M, N] (dL/d output) -> dx [M, K] (dx_dtype), dW [N, K] f32, db [N] f32.
+    bf16 compute: act', the bf16 GEMM operand and the bias gradient in one pass
+    (comet_act_bwd_colsum); x2 was saved in bf16 by the forward."""
+    M, N = dy2.shape
     K = x2.shape[1]
     dx = dw = db = None
-    if need_db:
-        db = ops.colsum(dpre)
-    dpc = dpre if dpre.dtype == wc.dtype else ops.cast(dpre, wc.dtype)
+    cdt = wc.dtype
+    if cdt == torch.bfloat16 and _vec8(dy2) and (aux is None or _vec8(aux)):
+        if need_db:
+            db = torch.empty(N, device=dy2.device, dtype=torch.float32)
+        if act != L.ACT_NONE or dy2.dtype != torch.bfloat16:
+            # one pass: act' (if any), bf16 GEMM operand, bias gradient
+            dpre = ops.act_bwd_colsum(act, aux, dy2, out_dtype=torch.bfloat16, dbias=db)
+        else:
+            dpre = dy2
+            if need_db:
+                ops.act_bwd_colsum(L.ACT_NONE, None, dy2, dbias=db, want_out=False)
+    else:
+        dpre = ops.act_bwd(act, aux, dy2, out_dtype=torch.float32) if act != L.ACT_NONE else dy2
+        if need_db:
+            db = ops.colsum(dpre)
+        if dpre.dtype != cdt:
+            dpre = ops.cast(dpre, cdt)
     if need_dx:
-        dx = torch.empty(M, K, device=dpre.device, dtype=dx_dtype)
-        ops.gemm_raw(dpc, wc, dx, m=M, n=K, k=N, layout_a=0, lda=dpc.stride(0), layout_b=1,
-                     ldb=wc.stride(0), ldc=K)
+        dx = torch.empty(M, K, device=dy2.device, dtype=dx_dtype)
+        ops.gemm_raw(dpre, wc, dx, m=M, n=K, k=N, layout_a=0, lda=dpre.stride(0), layout_b=1,
+                     ldb=wc.stride(0), ldc=K, compute=cdt)
     if need_dw:
-        xc = x2 if x2.dtype == wc.dtype else ops.cast(x2, wc.dtype)
-        dw = torch.empty(N, K, device=dpre.device, dtype=torch.float32)
-        ops.gemm_raw(dpc, xc, dw, m=N, n=K, k=M, layout_a=1, lda=dpc.stride(0), layout_b=1,
-                     ldb=xc.stride(0), ldc=K)
+        xc = x2 if (x2.dtype == cdt or cdt == torch.bfloat16) else ops.cast(x2, cdt)
+        dw = torch.empty(N, K, device=dy2.device, dtype=torch.float32)
+        ops.gemm_raw(dpre, xc, dw, m=N, n=K, k=M, layout_a=1, lda=dpre.stride(0), layout_b=1,
+                     ldb=xc.stride(0), ldc=K, compute=cdt)
     return dx, dw, db
 
 
@@ -152,13 +172,14 @@ class _Linear(torch.autograd.Function):
         dy2 = dy.reshape(-1, N)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dpre = ops.act_bwd(ctx.act, aux, dy2, out_dtype=torch.float32) if ctx.act != L.ACT_NONE else dy2
         wc = wcast(w, ctx.cdt)
-        dx, dw, db = _linear_bwd(x2, wc, dpre, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                                 ctx.has_b and ctx.needs_input_grad[2], torch.float32)
+        # dx straight in the input's dtype (the reference's autocast grad of a bf16 tensor is bf16)
+        dx_dtype = ctx.xdtype if ctx.cdt == torch.bfloat16 else torch.float32
+        dx, dw, db = _linear_bwd(x2, wc, dy2, ctx.act, aux, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
+                                 ctx.has_b and ctx.needs_input_grad[2], dx_dtype)
         if dx is not None:
             dx = dx.reshape(ctx.shape)
-            if ctx.xdtype != torch.float32:
+            if dx.dtype != ctx.xdtype:
                 dx = ops.cast(dx, ctx.xdtype)
         dres = None
         if ctx.has_r and ctx.needs_input_grad[3]:
@@ -181,8 +202,8 @@ def linear(x, w, b=None, act=L.ACT_NONE, resid=None, beta=1.0, out_dtype=None):
 # ------------------------------------------------------------------------------------------
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, eps):
-        y, mean, rstd = ops.layernorm(x, w, b, eps=eps, out_dtype=torch.float32, stats=True)
+    def forward(ctx, x, w, b, eps, out_dtype):
+        y, mean, rstd = ops.layernorm(x, w, b, eps=eps, out_dtype=out_dtype, stats=True)
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.has_w, ctx.has_b = w is not None, b is not None
         return y
@@ -193,16 +214,49 @@ class _LayerNorm(torch.autograd.Function):
         C = x.shape[-1]
         dw = torch.zeros(C, device=x.device) if ctx.has_w and ctx.needs_input_grad[1] else None
         db = torch.zeros(C, device=x.device) if ctx.has_b and ctx.needs_input_grad[2] else None
-        dx = ops.layernorm_bwd(x, dy, mean, rstd, w, dw, db)
-        if x.dtype != torch.float32:
-            dx = ops.cast(dx, x.dtype)
-        return dx, dw, db, None
+        dx = ops.layernorm_bwd(x, dy, mean, rstd, w, dw, db, dx_dtype=x.dtype)
+        return dx, dw, db, None, None
 
 
-def layer_norm(x, w=None, b=None, eps=1e-5):
+class _LayerNormDual(torch.autograd.Function):
+    """LN whose output feeds both an f32 residual and a bf16 GEMM (AttnBlock / CrossAttnBlock
+    norm1: the reference adds the attention output to the NORMED x, modules.py:290-293): one
+    kernel writes both copies, backward sums both incoming gradients in the LN kernel."""
+
+    @staticmethod
+    def forward(ctx, x, eps):
+        y, y16, mean, rstd = ops.layernorm(x, None, None, eps=eps, out_dtype=torch.float32, stats=True, dual=True)
+        ctx.save_for_backward(x, mean, rstd)
+        return y, y16
+
+    @staticmethod
+    def backward(ctx, dy, dy16):
+        x, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dy, dy16 = dy16, None
+        if dy is None:
+            return None, None
+        dx = ops.layernorm_bwd(x, dy, mean, rstd, dy2=dy16, dx_dtype=x.dtype)
+        return dx, None
+
+
+def layer_norm(x, w=None, b=None, eps=1e-5, out_dtype=torch.float32):
+    """nn.LayerNorm; out_dtype = compute dtype when the output only feeds a GEMM (the reference's
+    autocast rounds it to bf16 at the Linear anyway)."""
     if _needs_grad(x, w, b):
-        return _LayerNorm.apply(x, w, b, eps)
-    return ops.layernorm(x, w, b, eps=eps, out_dtype=torch.float32)
+        return _LayerNorm.apply(x, w, b, eps, out_dtype)
+    return ops.layernorm(x, w, b, eps=eps, out_dtype=out_dtype)
+
+
+def layer_norm_dual(x, eps=1e-5):
+    """(y f32, y in the compute dtype) of a non-affine LN: residual copy + GEMM operand."""
+    if compute_dtype() != torch.bfloat16:
+        y = layer_norm(x, eps=eps)
+        return y, y
+    if _needs_grad(x):
+        return _LayerNormDual.apply(x, eps)
+    y, y16 = ops.layernorm(x, eps=eps, out_dtype=torch.float32, dual=True)
+    return y, y16
 
 
 # ------------------------------------------------------------------------------------------
@@ -279,7 +333,11 @@ class _Attention(torch.autograd.Function):
         dqsrc = torch.empty_like(qsrc)
         dkvsrc = None if kvsrc is None else torch.empty_like(kvsrc)
         dq, dk, dv = _split(dqsrc, dkvsrc, C)
-        _attn_bwd(q, k, v, o, lse, do, ctx.heads, ctx.scale, dq, dk, dv)
+        if ops.attention_bwd_ok(q, k, v, o, do, ctx.heads) and all(t.data_ptr() % 16 == 0 and t.stride(1) % 8 == 0
+                                                                    for t in (dq, dk, dv)):
+            ops.attention_bwd(q, k, v, o, lse, do, ctx.heads, ctx.scale, dq, dk, dv)
+        else:  # f32 (parity precision) or unsupported head size: materialised backward
+            _attn_bwd(q, k, v, o, lse, do, ctx.heads, ctx.scale, dq, dk, dv)
         return dqsrc, dkvsrc, None, None, None
 
 

@@ -51,11 +51,11 @@ class AttnBlock(nn.Module):
     def forward(self, x, mask=None):
         C = x.shape[-1]
         a = self.attn
-        x = F.layer_norm(x, eps=1e-6)
-        qkv = F.linear(x, a.in_proj_weight, a.in_proj_bias)
+        x, xc = F.layer_norm_dual(x, eps=1e-6)  # residual is the normed x (modules.py:290)
+        qkv = F.linear(xc, a.in_proj_weight, a.in_proj_bias)
         o = F.attention(qkv, None, self.heads, C)
         x = F.linear(o, a.out_proj.weight, a.out_proj.bias, resid=x, out_dtype=torch.float32)
-        return self.mlp(F.layer_norm(x, eps=1e-6), resid=x)
+        return self.mlp(F.layer_norm(x, eps=1e-6, out_dtype=F.compute_dtype()), resid=x)
 
 
 class CrossAttnBlock(nn.Module):
@@ -71,14 +71,15 @@ class CrossAttnBlock(nn.Module):
     def forward(self, x, context, mask=None):
         C = x.shape[-1]
         a = self.cross_attn
-        x = F.layer_norm(x, eps=1e-6)
-        ctx = F.layer_norm(context, self.norm_context.weight, self.norm_context.bias, eps=1e-5)
+        x, xc = F.layer_norm_dual(x, eps=1e-6)
+        ctx = F.layer_norm(context, self.norm_context.weight, self.norm_context.bias, eps=1e-5,
+                           out_dtype=F.compute_dtype())
         W, b = a.in_proj_weight, a.in_proj_bias
-        q = F.linear(x, W[:C], b[:C])
+        q = F.linear(xc, W[:C], b[:C])
         kv = F.linear(ctx, W[C:], b[C:])
         o = F.attention(q, kv, self.heads, C)
         x = F.linear(o, a.out_proj.weight, a.out_proj.bias, resid=x, out_dtype=torch.float32)
-        return self.mlp(F.layer_norm(x, eps=1e-6), resid=x)
+        return self.mlp(F.layer_norm(x, eps=1e-6, out_dtype=F.compute_dtype()), resid=x)
 
 
 # ------------------------------------------------------------------------------------------

@@ -40,17 +40,34 @@ def _req_cuda(*ts):
 def gemm_raw(a, b, c, *, m, n, k, layout_a, lda, layout_b, ldb, ldc, batch=(1, 1),
              stride_a=(0, 0), stride_b=(0, 0), stride_c=(0, 0), bias=None, bias_mode=0,
              stride_bias=(0, 0), resid=None, ldr=0, stride_r=(0, 0), beta=1.0, aux=None,
-             ldaux=0, stride_aux=(0, 0), alpha=1.0, act=L.ACT_NONE, split_k=0):
+             ldaux=0, stride_aux=(0, 0), alpha=1.0, act=L.ACT_NONE, split_k=0, compute=None):
     _req_cuda(a, b, c, bias, resid, aux)
-    if a.dtype != b.dtype:
-        raise L.CometHipError("gemm: A and B must share a dtype")
+    conv_a = conv_b = 0
+    cdt = compute or (a.dtype if a.dtype == b.dtype else torch.bfloat16)
+    if cdt == torch.bfloat16:
+        # f32 operands of a bf16 GEMM are rounded to bf16 on load when their rows allow 16-B
+        # vectors (convert_b: layout_b 1 only), otherwise by a cast pass here
+        if a.dtype == torch.float32:
+            if _cvt_ok(a, lda, stride_a, k if layout_a == 0 else m):
+                conv_a = 1
+            else:
+                a = _dense_bf16(a)
+        if b.dtype == torch.float32:
+            if layout_b == 1 and _cvt_ok(b, ldb, stride_b, n):
+                conv_b = 1
+            else:
+                b = _dense_bf16(b)
+    elif a.dtype != torch.float32 or b.dtype != torch.float32:
+        raise L.CometHipError("gemm: an f32 GEMM needs f32 operands")
     if bias is not None and bias.dtype != torch.float32:
         raise L.CometHipError("gemm: bias must be f32")
     for t in (resid, aux):
         if t is not None and t.dtype != c.dtype:
             raise L.CometHipError("gemm: resid/aux must have the output dtype")
     g = L.GemmArgs()
-    g.dtype_ab, g.dtype_c, g.layout_a, g.layout_b = dt(a), dt(c), layout_a, layout_b
+    g.dtype_ab = _DT[cdt]
+    g.dtype_c, g.layout_a, g.layout_b = dt(c), layout_a, layout_b
+    g.convert_a, g.convert_b = conv_a, conv_b
     g.m, g.n, g.k = m, n, k
     g.batch[0], g.batch[1] = batch
     g.a, g.lda = _p(a), lda
@@ -83,6 +100,19 @@ def gemm_raw(a, b, c, *, m, n, k, layout_a, lda, layout_b, ldb, ldc, batch=(1, 1
                     f" act{act}{' bias' if bias is not None else ''}{' res' if resid is not None else ''}")
         PROF.stop(e0, name, 2.0 * m * n * k * batch[0] * batch[1])
     return c
+
+
+def _cvt_ok(t, ld, st, contig):
+    return t.data_ptr() % 16 == 0 and ld % 8 == 0 and st[0] % 8 == 0 and st[1] % 8 == 0 and contig % 8 == 0
+
+
+def _dense_bf16(t):
+    """bf16 copy of an f32 GEMM operand that cannot be converted on load (same strides)."""
+    if t.is_contiguous():
+        return cast(t, torch.bfloat16)
+    out = torch.empty_strided(t.shape, t.stride(), device=t.device, dtype=torch.bfloat16)
+    out.copy_(t)  # rare misaligned view; keeps the caller's ld / strides valid
+    return out
 
 
 def linear(x, w, bias=None, act=L.ACT_NONE, resid=None, out=None, out_dtype=None, aux=None,
@@ -139,7 +169,10 @@ def _rows2d(x):
     return rows, ld
 
 
-def layernorm(x, weight=None, bias=None, eps=1e-5, out_dtype=None, stats=False, out=None, relu=False):
+def layernorm(x, weight=None, bias=None, eps=1e-5, out_dtype=None, stats=False, out=None, relu=False,
+              dual=False):
+    """Row LayerNorm. dual=True also returns a bf16 copy of the output (written by the same
+    kernel): (y, y_bf16[, mean, rstd])."""
     _req_cuda(x)
     C = x.shape[-1]
     r = _rows2d(x)
@@ -152,29 +185,34 @@ def layernorm(x, weight=None, bias=None, eps=1e-5, out_dtype=None, stats=False, 
     ry = _rows2d(y)
     if ry is None:
         raise L.CometHipError("layernorm: output rows must be uniformly strided")
+    y2 = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16) if dual else None
     mean = rstd = None
     if stats:
         mean = torch.empty(rows, device=x.device, dtype=torch.float32)
         rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
-    L.check(L.load().comet_layernorm_fwd(dt(xc), dt(y), _p(xc), _p(weight), _p(bias), _p(y), _p(mean),
-                                         _p(rstd), rows, C, ldx, ry[1], float(eps), int(relu), stream()),
+    L.check(L.load().comet_layernorm_fwd(dt(xc), dt(y), _p(xc), _p(weight), _p(bias), _p(y), _p(y2), _p(mean),
+                                         _p(rstd), rows, C, ldx, ry[1], C, float(eps), int(relu), stream()),
             "layernorm")
+    outs = (y, y2) if dual else (y,)
     if stats:
-        return y, mean, rstd
-    return y
+        outs = outs + (mean, rstd)
+    return outs if len(outs) > 1 else y
 
 
-def layernorm_bwd(x, dy, mean, rstd, weight=None, dweight=None, dbias=None, dx=None, accumulate=False):
+def layernorm_bwd(x, dy, mean, rstd, weight=None, dweight=None, dbias=None, dx=None, accumulate=False, dy2=None,
+                  dx_dtype=torch.float32):
+    """dx = LN backward of dy (+ dy2, bf16); dweight/dbias accumulated."""
     C = x.shape[-1]
     rows = x.numel() // C
     xc = x.contiguous()
     dyc = dy.contiguous()
+    dy2c = dy2.contiguous() if dy2 is not None else None
     if dx is None:
-        dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+        dx = torch.empty(x.shape, device=x.device, dtype=dx_dtype)
         accumulate = False
-    L.check(L.load().comet_layernorm_bwd(dt(xc), dt(dyc), _p(xc), _p(dyc), _p(mean), _p(rstd), _p(weight),
-                                         _p(dx), _p(dweight), _p(dbias), rows, C, int(accumulate),
-                                         stream()), "layernorm_bwd")
+    L.check(L.load().comet_layernorm_bwd(dt(xc), dt(dyc), _p(xc), _p(dyc), _p(dy2c), _p(mean), _p(rstd),
+                                         _p(weight), dt(dx), _p(dx), _p(dweight), _p(dbias), rows, C,
+                                         int(accumulate), stream()), "layernorm_bwd")
     return dx
 
 
@@ -205,8 +243,45 @@ def attention(q, k, v, heads, scale=None, out=None, lse=False):
     a.lse, a.scale = _p(lse_t), float(scale)
     e0 = PROF.start()
     L.check(L.load().comet_attention_fwd(ctypes.byref(a), stream()), "attention")
-    PROF.stop(e0, "comet_attention_fwd", 4.0 * B * heads * Lq * Lk * D)
+    if e0 is not None:
+        name = f"attn fwd B{B} H{heads} Lq{Lq} Lk{Lk} D{D}" if PROF.detail else "comet_attention_fwd"
+        PROF.stop(e0, name, 4.0 * B * heads * Lq * Lk * D)
     return (out, lse_t) if lse else out
+
+
+def attention_bwd(q, k, v, o, lse, do, heads, scale, dq, dk, dv):
+    """Fused bf16 attention backward (comet_attention_bwd). All tensors are token-major views
+    [B, L, H*D] with unit-stride last dim; dq/dk/dv may be strided slices of packed buffers."""
+    _req_cuda(q, k, v, o, do, dq, dk, dv, lse)
+    B, Lq, C = q.shape
+    Lk = k.shape[1]
+    D = C // heads
+    delta = torch.empty(B, heads, Lq, device=q.device, dtype=torch.float32)
+    a = L.AttnBwdArgs()
+    a.dtype, a.head_dim = dt(q), D
+    a.batch, a.heads, a.lq, a.lk = B, heads, Lq, Lk
+    for name, t in (("q", q), ("k", k), ("v", v), ("o", o), ("d", do), ("dq", dq), ("dk", dk), ("dv", dv)):
+        if t.stride(2) != 1:
+            raise L.CometHipError("attention_bwd: head dim must be unit-stride")
+        field = "dout" if name == "d" else name
+        setattr(a, field, _p(t))
+        setattr(a, f"s{name}_b", t.stride(0))
+        setattr(a, f"s{name}_h", D)
+        setattr(a, f"s{name}_l", t.stride(1))
+    a.lse, a.delta, a.scale = _p(lse), _p(delta), float(scale)
+    e0 = PROF.start()
+    L.check(L.load().comet_attention_bwd(ctypes.byref(a), stream()), "attention_bwd")
+    if e0 is not None:
+        name = f"attn bwd B{B} H{heads} Lq{Lq} Lk{Lk} D{D}" if PROF.detail else "comet_attention_bwd"
+        PROF.stop(e0, name, 10.0 * B * heads * Lq * Lk * D)
+
+
+def attention_bwd_ok(q, k, v, o, do, heads):
+    D = q.shape[-1] // heads
+    ts = (q, k, v, o, do)
+    return (q.dtype == torch.bfloat16 and D in (32, 48, 64, 96) and all(t.dtype == torch.bfloat16 for t in ts)
+            and all(t.stride(2) == 1 and t.stride(0) % 8 == 0 and t.stride(1) % 8 == 0 and t.data_ptr() % 16 == 0
+                    for t in ts))
 
 
 # ------------------------------------------------------------------------------------------
@@ -225,6 +300,18 @@ def act_bwd(act, pre, dy, out_dtype=None):
     L.check(L.load().comet_act_bwd(act, dt(pre), dt(dyc), _p(pre), _p(dyc), _p(dx), dt(dx), pre.numel(),
                                    stream()), "act_bwd")
     return dx
+
+
+def act_bwd_colsum(act, pre, dy, out_dtype=None, dbias=None, accumulate=False, want_out=True):
+    """One pass: g = dy * act'(pre) -> out (out_dtype) and dbias (+)= column sums of g.
+    dy [rows, cols] contiguous; pre same shape (ignored for ACT_NONE)."""
+    rows, cols = dy.shape
+    out = torch.empty(rows, cols, device=dy.device, dtype=out_dtype or dy.dtype) if want_out else None
+    pre_p = _p(pre) if act != L.ACT_NONE else None
+    L.check(L.load().comet_act_bwd_colsum(act, dt(pre) if pre is not None else 0, pre_p, dt(dy), _p(dy),
+                                          dt(out) if out is not None else 0, _p(out), _p(dbias), rows, cols,
+                                          int(accumulate), stream()), "act_bwd_colsum")
+    return out
 
 
 def colsum(x2d, out=None, accumulate=False):
@@ -514,3 +601,39 @@ def harmonic_bwd(x, freqs, append_input, dy, diag_cov=None):
     _chk(L.load().comet_harmonic_bwd(_p(xc), _p(cov), _p(freqs), _p(dyc), _p(dx), _p(dcov), rows, dim, n,
                                      int(append_input), stream()), "harmonic_bwd")
     return dx, dcov
+
+
+# ------------------------------------------------------------------------------------------
+# per-call-site timing for tools/gemm_shapes.py (PROF.detail): every op below is bracketed
+# with HIP events and keyed by op name, tensor shapes and the calling model line.
+# ------------------------------------------------------------------------------------------
+def _timed(fn):
+    import functools
+    import os
+    import sys
+
+    @functools.wraps(fn)
+    def wrap(*args, **kwargs):
+        if not (PROF.enabled and PROF.detail):
+            return fn(*args, **kwargs)
+        f = sys._getframe(1)
+        while f is not None and f.f_code.co_filename.endswith("ops.py"):
+            f = f.f_back
+        sites = []
+        while f is not None and len(sites) < 2:
+            sites.append(f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}")
+            f = f.f_back
+        site = "<".join(sites) or "?"
+        shapes = ",".join("x".join(map(str, a.shape)) + str(a.dtype)[6:] for a in args if isinstance(a, torch.Tensor))
+        e0 = PROF.start()
+        out = fn(*args, **kwargs)
+        PROF.stop(e0, f"{fn.__name__} [{shapes}] @{site}")
+        return out
+    return wrap
+
+
+for _name in ("layernorm", "layernorm_bwd", "cast", "act_bwd", "colsum", "act_bwd_colsum", "instnorm_nhwc", "resize_bilinear",
+              "im2col_nhwc", "act_fwd", "binary", "add_rows", "rowscale", "rowscale_bwd", "sample_bilinear",
+              "corr_sample", "tracker_tokens", "coords_update", "avgpool2_nhwc", "patch_gather", "refine_combine",
+              "track_score", "dino_prep", "pose_encode", "pose_decode"):
+    globals()[_name] = _timed(globals()[_name])

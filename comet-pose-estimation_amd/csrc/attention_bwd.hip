@@ -1,0 +1,391 @@
+// Fused multi-head attention backward (flash style, bf16) -- comet_attention_bwd.
+//
+// Replaces the autograd backward of nn.MultiheadAttention's softmax(q kᵀ·scale)·v
+//  for the camera head's self / cross-frame / T_P / trunk attention
+// (camera_predictor10.py:329-348, 365-382, 663-683): nothing of size Lq x Lk reaches HBM.
+//
+//   P = exp(S - lse),  S = scale·Q Kᵀ        (lse from the forward)
+//   dV = Pᵀ dO,  dP = dO Vᵀ,  dS = P ∘ (dP - Δ),  Δ_q = Σ_d dO·O
+//   dQ = scale·dS K,  dK = scale·dSᵀ Q
+//
+// Two kernels, no atomics:
+//  * dkdv: one workgroup per 64 keys (4 waves x 16 keys, K/V fragments in registers), walks all
+//    query tiles; S and dP are computed with the query on the MFMA row so P / dS land in exactly
+//    the register layout of an A operand for dV += Pᵀ·dO and dK += dSᵀ·Q, whose B operands
+//    (dO, Q columns) come from the LDS tile by ds_read_b64_tr_b16.
+//  * dq: one workgroup per 64 queries, structured like the forward (Sᵀ = K·Qᵀ with the query on
+//    the lane), adds dPᵀ = V·dOᵀ and accumulates dQᵀ += Kᵀ·dSᵀ with Kᵀ fragments read by
+//    ds_read_b64_tr_b16.
+// The k index of the P/dS operands is permuted (32u + 4g + j, 32u + 16 + 4g + j) identically
+// on both MFMA operands, as in the forward's P·V.
+#include "common.hpp"
+
+namespace comet {
+namespace {
+
+constexpr float LOG2E_B = 1.4426950408889634f;
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4b;
+
+template <int D> struct BCfg {
+  static constexpr int DA = ((D + 31) / 32) * 32;  // k-dim of Q·Kᵀ (x32, zero padded)
+  static constexpr int KP = DA + 8;                 // LDS row pitch (bf16 elements)
+  static constexpr int NQC = DA / 32;               // 32-deep MFMA steps over d
+  static constexpr int DT = D / 16;                 // 16-wide output tiles over d
+  static constexpr int NVROW = D / 8;               // 16-B vectors per row
+  static constexpr int NVT = (64 * NVROW + 255) / 256;
+};
+
+__device__ __forceinline__ bf16x8 frag_rows(const __bf16* base, int row, int col) {
+  return *reinterpret_cast<const bf16x8*>(base + row + col);
+}
+
+// 4 consecutive d of rows r0+{0..3} (lane's column) for both k halves: the B / A operand with the
+// permuted k order (rows 32u + 4g + qq and 32u + 16 + 4g + qq of a [64][KP] tile)
+template <int KP>
+__device__ __forceinline__ bf16x8 frag_tr(const __bf16* tile, int u, int g, int qq, int pp, int col0) {
+  const __bf16* a0 = tile + (32 * u + 4 * g + qq) * KP + col0 + 4 * pp;
+  const __bf16* a1 = tile + (32 * u + 16 + 4 * g + qq) * KP + col0 + 4 * pp;
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4b*)(a0));
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4b*)(a1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__device__ __forceinline__ bf16x8 pack_operand(const f32x4& lo, const f32x4& hi) {
+  const bf16x4 p0 = __builtin_convertvector(lo, bf16x4);
+  const bf16x4 p1 = __builtin_convertvector(hi, bf16x4);
+  return __builtin_shufflevector(p0, p1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+struct BwdPtrs {
+  const __bf16* q; int64_t sq_b, sq_h, sq_l;
+  const __bf16* k; int64_t sk_b, sk_h, sk_l;
+  const __bf16* v; int64_t sv_b, sv_h, sv_l;
+  const __bf16* dout; int64_t sd_b, sd_h, sd_l;
+  __bf16* dq; int64_t sdq_b, sdq_h, sdq_l;
+  __bf16* dk; int64_t sdk_b, sdk_h, sdk_l;
+  __bf16* dv; int64_t sdv_b, sdv_h, sdv_l;
+  const float* lse; const float* delta;
+  int heads, lq, lk; float scale;
+};
+
+// Load one 16-row x D register fragment set (row = lane & 15, d = 32c + 8g + j) from global.
+template <int D>
+__device__ __forceinline__ void load_frags(const __bf16* base, int64_t sl, int row, bool ok, int g,
+                                           bf16x8 (&f)[BCfg<D>::NQC]) {
+#pragma unroll
+  for (int c = 0; c < BCfg<D>::NQC; ++c) {
+    const int d0 = 32 * c + 8 * g;
+    f[c] = (ok && d0 < D) ? *reinterpret_cast<const bf16x8*>(base + (int64_t)row * sl + d0) : bf16x8{};
+  }
+}
+
+// ---------------------------------------------------------------- dK, dV
+template <int D>
+__global__ void __launch_bounds__(256)
+attn_bwd_dkdv_kernel(BwdPtrs p) {
+  typedef BCfg<D> C;
+  constexpr int KP = C::KP, NQC = C::NQC, DT = C::DT, NVROW = C::NVROW, NVT = C::NVT;
+  __shared__ __attribute__((aligned(16))) __bf16 Qs[64 * KP];
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[64 * KP];  // dO tile
+  __shared__ float lse_s[64], dl_s[64];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, qq = li >> 2, pp = li & 3;
+  const int64_t bh = blockIdx.y, b = bh / p.heads, h = bh % p.heads;
+  const __bf16* Q = p.q + b * p.sq_b + h * p.sq_h;
+  const __bf16* K = p.k + b * p.sk_b + h * p.sk_h;
+  const __bf16* V = p.v + b * p.sv_b + h * p.sv_h;
+  const __bf16* G = p.dout + b * p.sd_b + h * p.sd_h;
+  const float* LSE = p.lse + bh * p.lq;
+  const float* DL = p.delta + bh * p.lq;
+  const float sl2 = p.scale * LOG2E_B;
+
+  for (int i = tid; i < 64 * KP; i += 256) { Qs[i] = __bf16(0.f); Gs[i] = __bf16(0.f); }
+
+  const int key = blockIdx.x * 64 + wid * 16 + li;
+  bf16x8 kf[NQC], vf[NQC];
+  load_frags<D>(K, p.sk_l, key, key < p.lk, g, kf);
+  load_frags<D>(V, p.sv_l, key, key < p.lk, g, vf);
+
+  f32x4 dv[DT], dk[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) { dv[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+  uint4 qreg[NVT], greg[NVT];
+  float lreg = 0.f, dreg = 0.f;
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NVT; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / NVROW, cv = (idx % NVROW) * 8;
+      const int q = t * 64 + row;
+      if (idx < 64 * NVROW && q < p.lq) {
+        qreg[i] = *reinterpret_cast<const uint4*>(Q + (int64_t)q * p.sq_l + cv);
+        greg[i] = *reinterpret_cast<const uint4*>(G + (int64_t)q * p.sd_l + cv);
+      } else {
+        qreg[i] = uint4{0, 0, 0, 0};
+        greg[i] = uint4{0, 0, 0, 0};
+      }
+    }
+    if (tid < 64) {
+      const int q = t * 64 + tid;
+      lreg = q < p.lq ? LSE[q] * LOG2E_B : INFINITY;  // invalid queries: P = 0
+      dreg = q < p.lq ? DL[q] : 0.f;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < NVT; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < 64 * NVROW) {
+        const int row = idx / NVROW, cv = (idx % NVROW) * 8;
+        *reinterpret_cast<uint4*>(Qs + row * KP + cv) = qreg[i];
+        *reinterpret_cast<uint4*>(Gs + row * KP + cv) = greg[i];
+      }
+    }
+    if (tid < 64) { lse_s[tid] = lreg; dl_s[tid] = dreg; }
+  };
+
+  const int ntiles = (p.lq + 63) / 64;
+  gload(0);
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (t + 1 < ntiles) gload(t + 1);
+
+    // S, dP with the query on the row: C[q = 16st + 4g + r][key = li]
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      s[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NQC; ++c) {
+        const bf16x8 qa = frag_rows(Qs, (st * 16 + li) * KP, 32 * c + 8 * g);
+        const bf16x8 ga = frag_rows(Gs, (st * 16 + li) * KP, 32 * c + 8 * g);
+        s[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[c], s[st], 0, 0, 0);
+        dp[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, vf[c], dp[st], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ql = st * 16 + 4 * g + r;
+        const float pr = exp2f(s[st][r] * sl2 - lse_s[ql]);
+        s[st][r] = pr;                          // P
+        dp[st][r] = pr * (dp[st][r] - dl_s[ql]);  // dS (unscaled)
+      }
+    }
+    // dV += Pᵀ dO, dK += dSᵀ Q   (k = queries, permuted order)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8 pa = pack_operand(s[2 * u], s[2 * u + 1]);
+      const bf16x8 da = pack_operand(dp[2 * u], dp[2 * u + 1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const bf16x8 gb = frag_tr<KP>(Gs, u, g, qq, pp, 16 * dt);
+        const bf16x8 qb = frag_tr<KP>(Qs, u, g, qq, pp, 16 * dt);
+        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, gb, dv[dt], 0, 0, 0);
+        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, qb, dk[dt], 0, 0, 0);
+      }
+    }
+  }
+
+  // C layout: row = key 4g + r of the wave's 16, col = d 16dt + li
+  __bf16* dK = p.dk + b * p.sdk_b + h * p.sdk_h;
+  __bf16* dV = p.dv + b * p.sdv_b + h * p.sdv_h;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int kr = blockIdx.x * 64 + wid * 16 + 4 * g + r;
+    if (kr >= p.lk) continue;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      dV[(int64_t)kr * p.sdv_l + 16 * dt + li] = static_cast<__bf16>(dv[dt][r]);
+      dK[(int64_t)kr * p.sdk_l + 16 * dt + li] = static_cast<__bf16>(dk[dt][r] * p.scale);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- dQ
+template <int D>
+__global__ void __launch_bounds__(256)
+attn_bwd_dq_kernel(BwdPtrs p) {
+  typedef BCfg<D> C;
+  constexpr int KP = C::KP, NQC = C::NQC, DT = C::DT, NVROW = C::NVROW, NVT = C::NVT;
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[64 * KP];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[64 * KP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, qq = li >> 2, pp = li & 3;
+  const int64_t bh = blockIdx.y, b = bh / p.heads, h = bh % p.heads;
+  const __bf16* Q = p.q + b * p.sq_b + h * p.sq_h;
+  const __bf16* K = p.k + b * p.sk_b + h * p.sk_h;
+  const __bf16* V = p.v + b * p.sv_b + h * p.sv_h;
+  const __bf16* G = p.dout + b * p.sd_b + h * p.sd_h;
+  const float sl2 = p.scale * LOG2E_B;
+
+  for (int i = tid; i < 64 * KP; i += 256) { Ks[i] = __bf16(0.f); Vs[i] = __bf16(0.f); }
+
+  const int q = blockIdx.x * 64 + wid * 16 + li;
+  const bool qok = q < p.lq;
+  bf16x8 qf[NQC], gf[NQC];
+  load_frags<D>(Q, p.sq_l, q, qok, g, qf);
+  load_frags<D>(G, p.sd_l, q, qok, g, gf);
+  const float lse2 = qok ? p.lse[bh * p.lq + q] * LOG2E_B : INFINITY;
+  const float dl = qok ? p.delta[bh * p.lq + q] : 0.f;
+
+  f32x4 acc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 kreg[NVT], vreg[NVT];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NVT; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / NVROW, cv = (idx % NVROW) * 8;
+      const int kk = t * 64 + row;
+      if (idx < 64 * NVROW && kk < p.lk) {
+        kreg[i] = *reinterpret_cast<const uint4*>(K + (int64_t)kk * p.sk_l + cv);
+        vreg[i] = *reinterpret_cast<const uint4*>(V + (int64_t)kk * p.sv_l + cv);
+      } else {
+        kreg[i] = uint4{0, 0, 0, 0};
+        vreg[i] = uint4{0, 0, 0, 0};
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < NVT; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < 64 * NVROW) {
+        const int row = idx / NVROW, cv = (idx % NVROW) * 8;
+        *reinterpret_cast<uint4*>(Ks + row * KP + cv) = kreg[i];
+        *reinterpret_cast<uint4*>(Vs + row * KP + cv) = vreg[i];
+      }
+    }
+  };
+
+  const int ntiles = (p.lk + 63) / 64;
+  gload(0);
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (t + 1 < ntiles) gload(t + 1);
+
+    // Sᵀ, dPᵀ with the query on the lane: C[key = 16st + 4g + r][q = li]
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      s[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[st] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NQC; ++c) {
+        const bf16x8 ka = frag_rows(Ks, (st * 16 + li) * KP, 32 * c + 8 * g);
+        const bf16x8 va = frag_rows(Vs, (st * 16 + li) * KP, 32 * c + 8 * g);
+        s[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[c], s[st], 0, 0, 0);
+        dp[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, gf[c], dp[st], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kk = t * 64 + st * 16 + 4 * g + r;
+        const float pr = kk < p.lk ? exp2f(s[st][r] * sl2 - lse2) : 0.f;
+        dp[st][r] = pr * (dp[st][r] - dl);  // dS (unscaled)
+      }
+    }
+    // dQᵀ += Kᵀ dSᵀ  (k = keys, permuted order)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16x8 db = pack_operand(dp[2 * u], dp[2 * u + 1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const bf16x8 ka = frag_tr<KP>(Ks, u, g, qq, pp, 16 * dt);
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, db, acc[dt], 0, 0, 0);
+      }
+    }
+  }
+
+  if (!qok) return;
+  // C layout: row = d 16dt + 4g + r, col = query li
+  __bf16* dQ = p.dq + b * p.sdq_b + h * p.sdq_h + (int64_t)q * p.sdq_l;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const bf16x4 w = __builtin_convertvector(acc[dt] * p.scale, bf16x4);
+    *reinterpret_cast<bf16x4*>(dQ + 16 * dt + 4 * g) = w;
+  }
+}
+
+// Δ = rowsum(dO ∘ O), one wave per 4 query rows... one lane group of 8 per row (D <= 128)
+__global__ void __launch_bounds__(256)
+attn_delta_bf16_kernel(const __bf16* __restrict__ dO, const __bf16* __restrict__ O, float* __restrict__ delta,
+                       int heads, int lq, int D, int64_t so_b, int64_t so_h, int64_t so_l, int64_t sd_b,
+                       int64_t sd_h, int64_t sd_l, int64_t rows) {
+  const int64_t r = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int sub = threadIdx.x & 7;
+  float acc = 0.f;
+  if (r < rows) {
+    const int64_t bh = r / lq, qi = r % lq, b = bh / heads, h = bh % heads;
+    const __bf16* o = O + b * so_b + h * so_h + qi * so_l;
+    const __bf16* g = dO + b * sd_b + h * sd_h + qi * sd_l;
+    for (int d = sub * 8; d < D; d += 64) {
+      float x[8], y[8];
+      load8(o + d, x);
+      load8(g + d, y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc += x[e] * y[e];
+    }
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (r < rows && sub == 0) delta[r] = acc;
+}
+
+template <int D>
+int launch_bwd(const BwdPtrs& p, int64_t bh, hipStream_t s) {
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D>), dim3((unsigned)cdiv(p.lk, 64), (unsigned)bh), dim3(256), 0, s, p);
+  COMET_CHECK_LAUNCH("comet_attention_bwd (dk, dv)");
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D>), dim3((unsigned)cdiv(p.lq, 64), (unsigned)bh), dim3(256), 0, s, p);
+  COMET_CHECK_LAUNCH("comet_attention_bwd (dq)");
+  return COMET_OK;
+}
+
+}  // namespace
+}  // namespace comet
+
+using namespace comet;
+
+extern "C" int comet_attention_bwd(const comet_attn_bwd_args* args, void* stream) {
+  COMET_CHECK_ARG(args != nullptr, "comet_attention_bwd: null args");
+  const comet_attn_bwd_args& a = *args;
+  COMET_CHECK_ARG(a.dtype == COMET_BF16, "comet_attention_bwd: bf16 only (f32 uses the materialised backward)");
+  COMET_CHECK_ARG(a.q && a.k && a.v && a.o && a.dout && a.dq && a.dk && a.dv && a.lse && a.delta,
+                  "comet_attention_bwd: null tensor");
+  COMET_CHECK_ARG(a.batch > 0 && a.heads > 0 && a.lq > 0 && a.lk > 0 && a.lq < (1ll << 30) && a.lk < (1ll << 30),
+                  "comet_attention_bwd: bad sizes");
+  COMET_CHECK_ARG(a.batch * a.heads <= 65535, "comet_attention_bwd: batch*heads > 65535");
+  const int64_t strides[] = {a.sq_b, a.sq_h, a.sq_l, a.sk_b, a.sk_h, a.sk_l, a.sv_b, a.sv_h, a.sv_l,
+                             a.so_b, a.so_h, a.so_l, a.sd_b, a.sd_h, a.sd_l, a.sdq_b, a.sdq_h, a.sdq_l,
+                             a.sdk_b, a.sdk_h, a.sdk_l, a.sdv_b, a.sdv_h, a.sdv_l};
+  for (int64_t st : strides) COMET_CHECK_ARG(st % 8 == 0, "comet_attention_bwd: strides must be multiples of 8 elements");
+  COMET_CHECK_ARG(((uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v | (uintptr_t)a.o | (uintptr_t)a.dout |
+                   (uintptr_t)a.dq) % 16 == 0, "comet_attention_bwd: tensors must be 16-byte aligned");
+  hipStream_t s = as_stream(stream);
+  const int64_t bh = a.batch * a.heads, rows = bh * a.lq;
+  hipLaunchKernelGGL(attn_delta_bf16_kernel, dim3((unsigned)cdiv(rows, 32)), dim3(256), 0, s,
+                     (const __bf16*)a.dout, (const __bf16*)a.o, a.delta, (int)a.heads, (int)a.lq, (int)a.head_dim,
+                     a.so_b, a.so_h, a.so_l, a.sd_b, a.sd_h, a.sd_l, rows);
+  COMET_CHECK_LAUNCH("comet_attention_bwd (delta)");
+  BwdPtrs p{(const __bf16*)a.q, a.sq_b, a.sq_h, a.sq_l, (const __bf16*)a.k, a.sk_b, a.sk_h, a.sk_l,
+            (const __bf16*)a.v, a.sv_b, a.sv_h, a.sv_l, (const __bf16*)a.dout, a.sd_b, a.sd_h, a.sd_l,
+            (__bf16*)a.dq, a.sdq_b, a.sdq_h, a.sdq_l, (__bf16*)a.dk, a.sdk_b, a.sdk_h, a.sdk_l,
+            (__bf16*)a.dv, a.sdv_b, a.sdv_h, a.sdv_l, a.lse, a.delta, (int)a.heads, (int)a.lq, (int)a.lk, a.scale};
+  switch (a.head_dim) {
+    case 32: return launch_bwd<32>(p, bh, s);
+    case 48: return launch_bwd<48>(p, bh, s);
+    case 64: return launch_bwd<64>(p, bh, s);
+    case 96: return launch_bwd<96>(p, bh, s);
+    default: set_error("comet_attention_bwd: head_dim must be 32, 48, 64 or 96"); return COMET_EINVAL;
+  }
+}

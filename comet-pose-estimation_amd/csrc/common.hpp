@@ -66,6 +66,29 @@ __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
   reinterpret_cast<float4*>(p)[1] = float4{v[4], v[5], v[6], v[7]};
 }
 
+// 4-element variants (16 B of f32, 8 B of bf16)
+__device__ __forceinline__ void load4(const float* p, float (&v)[4]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+__device__ __forceinline__ void load4(const __bf16* p, float (&v)[4]) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = bf16_lo(u.x); v[1] = bf16_hi(u.x); v[2] = bf16_lo(u.y); v[3] = bf16_hi(u.y);
+}
+__device__ __forceinline__ void store4(float* p, const float (&v)[4]) {
+  *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ void store4(__bf16* p, const float (&v)[4]) {
+  *reinterpret_cast<uint2*>(p) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+}
+// N in {4, 8}
+template <int N, typename T> __device__ __forceinline__ void loadn(const T* p, float (&v)[N]) {
+  if constexpr (N == 4) load4(p, v); else load8(p, v);
+}
+template <int N, typename T> __device__ __forceinline__ void storen(T* p, const float (&v)[N]) {
+  if constexpr (N == 4) store4(p, v); else store8(p, v);
+}
+
 // ---- wave (64-lane) reductions ------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

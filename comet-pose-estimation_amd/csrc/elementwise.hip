@@ -32,6 +32,64 @@ __global__ void act_bwd_kernel(int act, const TP* __restrict__ pre, const TD* __
   }
 }
 
+__device__ __forceinline__ float act_grad(int act, float p) {
+  switch (act) {
+    case COMET_ACT_GELU: return gelu_erf_grad(p);
+    case COMET_ACT_RELU: return p > 0.f ? 1.f : 0.f;
+    case COMET_ACT_SIGMOID: { const float s = 1.f / (1.f + __expf(-p)); return s * (1.f - s); }
+    default: return 1.f;
+  }
+}
+
+// Linear-layer backward prologue in one pass over dY [rows, cols] (cols % 8 == 0):
+// g = dY * act'(pre) (or dY), optionally stored (out, any dtype), and dbias[c] += sum_r g.
+// Block = 32 column groups of 8 x 8 row lanes; partial column sums meet in LDS, one atomic per
+// column per block.
+template <typename TP, typename TD, typename TO>
+__global__ void __launch_bounds__(256)
+act_bwd_colsum_kernel(int act, const TP* __restrict__ pre, const TD* __restrict__ dy, TO* __restrict__ out,
+                      float* __restrict__ dbias, int64_t rows, int cols, int64_t chunk) {
+  __shared__ float red[8][256];
+  const int t = threadIdx.x, cl = t & 31, rl = t >> 5;
+  const int c0 = blockIdx.x * 256 + cl * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk;
+  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  if (c0 < cols) {
+    for (int64_t r = r0 + rl; r < r1; r += 8) {
+      float g[8];
+      load8(dy + r * cols + c0, g);
+      if (pre) {
+        float x[8];
+        load8(pre + r * cols + c0, x);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] *= act_grad(act, x[e]);
+      }
+      if (out) {
+        // round first so the bias gradient sums exactly the values the GEMMs consume
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g[e] = to_f32(from_f32<TO>(g[e]));
+        store8(out + r * cols + c0, g);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += g[e];
+    }
+  }
+  if (!dbias) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][cl * 8 + e] = acc[e];
+  __syncthreads();
+  const int col = blockIdx.x * 256 + t;
+  if (col < cols) {
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sum += red[q][t];
+    atomicAdd(dbias + col, sum);
+  }
+}
+
 __global__ void axpby_kernel(const float* __restrict__ x, float* __restrict__ y, float a, float b,
                              int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -161,6 +219,39 @@ extern "C" int comet_axpby(const float* x, float* y, float a, float b, int64_t n
   if (n == 0) return COMET_OK;
   hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, y, a, b, n);
   COMET_CHECK_LAUNCH("comet_axpby");
+  return COMET_OK;
+}
+
+extern "C" int comet_act_bwd_colsum(int act, int dtype_pre, const void* pre, int dtype_dy, const void* dy,
+                                    int dtype_out, void* out, float* dbias, int64_t rows, int64_t cols,
+                                    int accumulate, void* stream) {
+  COMET_CHECK_ARG(dy && rows >= 0 && cols > 0 && cols % 8 == 0 && cols < (1ll << 31),
+                  "comet_act_bwd_colsum: dy required, cols a positive multiple of 8");
+  COMET_CHECK_ARG(act == COMET_ACT_NONE || pre != nullptr, "comet_act_bwd_colsum: activation needs pre");
+  COMET_CHECK_ARG(((uintptr_t)pre | (uintptr_t)dy | (uintptr_t)out) % 32 == 0, "comet_act_bwd_colsum: 32-B alignment");
+  hipStream_t s = as_stream(stream);
+  if (dbias && !accumulate) {
+    hipError_t e = hipMemsetAsync(dbias, 0, cols * sizeof(float), s);
+    if (e != hipSuccess) { set_error("comet_act_bwd_colsum: memset failed"); return COMET_ELAUNCH; }
+  }
+  if (rows == 0) return COMET_OK;
+  const int64_t cblocks = cdiv(cols, 256);
+  int64_t rblocks = cdiv(2048, cblocks);                 // ~2048 workgroups
+  int64_t chunk = cdiv(rows, rblocks);
+  if (chunk < 64) chunk = 64;
+  rblocks = cdiv(rows, chunk);
+  COMET_CHECK_ARG(rblocks <= 65535, "comet_act_bwd_colsum: too many rows");
+  dim3 grid((unsigned)cblocks, (unsigned)rblocks);
+  const void* P = act == COMET_ACT_NONE ? nullptr : pre;
+#define ABC(TP, TD, TO) \
+  hipLaunchKernelGGL((act_bwd_colsum_kernel<TP, TD, TO>), grid, dim3(256), 0, s, act, (const TP*)P, (const TD*)dy, (TO*)out, dbias, rows, (int)cols, chunk)
+#define ABC_O(TP, TD) do { if (dtype_out == COMET_F32) ABC(TP, TD, float); else ABC(TP, TD, __bf16); } while (0)
+#define ABC_D(TP) do { if (dtype_dy == COMET_F32) ABC_O(TP, float); else ABC_O(TP, __bf16); } while (0)
+  if (dtype_pre == COMET_F32) ABC_D(float); else ABC_D(__bf16);
+#undef ABC_D
+#undef ABC_O
+#undef ABC
+  COMET_CHECK_LAUNCH("comet_act_bwd_colsum");
   return COMET_OK;
 }
 

@@ -197,39 +197,52 @@ __device__ __forceinline__ uint4 pack8(const unsigned short (&s)[8]) {
   return u;
 }
 
-// One operand's 128 x 64 tile, 4 x 16-B vectors per thread.
-template <int LAYOUT, bool VEC>
+// One operand's 128 x 64 tile, 4 x 16-B (8 x bf16) vectors per thread.
+// KIND 0: bf16, element loads (misaligned / ragged operands); 1: bf16, 16-B vector loads;
+// 2: f32 in memory, 2 x 16-B loads converted to bf16 (round to nearest even) in the staging
+//    registers -- the GEMM reads f32 activations / gradients without a separate cast pass.
+enum { K_BF16_SCALAR = 0, K_BF16_VEC = 1, K_F32_CVT = 2 };
+
+__device__ __forceinline__ uint4 cvt8(const float* p) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  return uint4{pack_bf16x2(a.x, a.y), pack_bf16x2(a.z, a.w), pack_bf16x2(b.x, b.y), pack_bf16x2(b.z, b.w)};
+}
+
+template <int LAYOUT, int KIND>
 struct Loader {
   uint4 reg[4];
 
-  __device__ __forceinline__ void load(const __bf16* __restrict__ base, int64_t ld, int64_t r0,
+  __device__ __forceinline__ void load(const void* __restrict__ base, int64_t ld, int64_t r0,
                                        int64_t rmax, int64_t k0, int64_t kmax) {
     const unsigned short* b16 = reinterpret_cast<const unsigned short*>(base);
+    const float* f32 = reinterpret_cast<const float*>(base);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int v = threadIdx.x + i * NT;
+      int64_t gr, gk, off;
+      bool ok;
       if (LAYOUT == 0) {
         const int row = v >> 3, kv = (v & 7) * 8;
-        const int64_t gr = r0 + row, gk = k0 + kv;
-        if (VEC) {
-          reg[i] = (gr < rmax && gk < kmax) ? *reinterpret_cast<const uint4*>(b16 + gr * ld + gk) : uint4{0, 0, 0, 0};
-        } else {
-          unsigned short s[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) s[e] = (gr < rmax && gk + e < kmax) ? b16[gr * ld + gk + e] : (unsigned short)0;
-          reg[i] = pack8(s);
-        }
+        gr = r0 + row; gk = k0 + kv;
+        off = gr * ld + gk;
       } else {
         const int krow = v >> 4, rv = (v & 15) * 8;
-        const int64_t gk = k0 + krow, gr = r0 + rv;
-        if (VEC) {
-          reg[i] = (gk < kmax && gr < rmax) ? *reinterpret_cast<const uint4*>(b16 + gk * ld + gr) : uint4{0, 0, 0, 0};
-        } else {
-          unsigned short s[8];
+        gk = k0 + krow; gr = r0 + rv;
+        off = gk * ld + gr;
+      }
+      ok = gr < rmax && gk < kmax;
+      if (KIND == K_BF16_VEC) {
+        reg[i] = ok ? *reinterpret_cast<const uint4*>(b16 + off) : uint4{0, 0, 0, 0};
+      } else if (KIND == K_F32_CVT) {
+        reg[i] = ok ? cvt8(f32 + off) : uint4{0, 0, 0, 0};
+      } else {
+        unsigned short s[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) s[e] = (gk < kmax && gr + e < rmax) ? b16[gk * ld + gr + e] : (unsigned short)0;
-          reg[i] = pack8(s);
+        for (int e = 0; e < 8; ++e) {
+          const bool oke = LAYOUT == 0 ? (gr < rmax && gk + e < kmax) : (gk < kmax && gr + e < rmax);
+          s[e] = oke ? b16[off + e] : (unsigned short)0;
         }
+        reg[i] = pack8(s);
       }
     }
   }
@@ -283,7 +296,7 @@ struct ConvLoader {
     }
   }
 
-  __device__ __forceinline__ void load(const __bf16*, int64_t, int64_t, int64_t, int64_t k0, int64_t kmax) {
+  __device__ __forceinline__ void load(const void*, int64_t, int64_t, int64_t, int64_t k0, int64_t kmax) {
     const int k = (int)k0 + (threadIdx.x & 7) * 8;
     const int tap = k / g.c, ci = k - tap * g.c;
     const int ky = tap / g.kw, kx = tap - ky * g.kw;
@@ -324,10 +337,10 @@ __device__ __forceinline__ bf16x8 frag(const __bf16* __restrict__ img, int rbase
   }
 }
 
-template <typename TC, int LA, int LB, bool VA, bool VB, bool SPLIT, bool CONV = false>
+template <typename TC, int LA, int LB, int KA, int KB, bool SPLIT, bool CONV = false>
 __global__ void __launch_bounds__(NT, 2)
-gemm_bf16_kernel(const __bf16* __restrict__ A, int64_t lda, int64_t sa0, int64_t sa1,
-                 const __bf16* __restrict__ B, int64_t ldb, int64_t sb0, int64_t sb1,
+gemm_bf16_kernel(const void* __restrict__ A, int64_t lda, int64_t sa0, int64_t sa1,
+                 const void* __restrict__ B, int64_t ldb, int64_t sb0, int64_t sb1,
                  TC* __restrict__ C, int64_t ldc, int64_t sc0, int64_t sc1,
                  int64_t M, int64_t N, int64_t K, int64_t nb1, int tiles_n, Epi epi, Split sp,
                  ConvGeo geo = ConvGeo{}) {
@@ -336,8 +349,8 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int64_t lda, int64_t sa0, int64_t
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int64_t bz = blockIdx.y, b0 = bz / nb1, b1 = bz % nb1;
-  A += b0 * sa0 + b1 * sa1;
-  B += b0 * sb0 + b1 * sb1;
+  A = reinterpret_cast<const char*>(A) + (b0 * sa0 + b1 * sa1) * (KA == K_F32_CVT ? 4 : 2);
+  B = reinterpret_cast<const char*>(B) + (b0 * sb0 + b1 * sb1) * (KB == K_F32_CVT ? 4 : 2);
   C += b0 * sc0 + b1 * sc1;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   int64_t kbeg = 0, kend = K;
@@ -355,8 +368,8 @@ gemm_bf16_kernel(const __bf16* __restrict__ A, int64_t lda, int64_t sa0, int64_t
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  typename std::conditional<CONV, ConvLoader, Loader<LA, VA>>::type la;
-  Loader<LB, VB> lb;
+  typename std::conditional<CONV, ConvLoader, Loader<LA, KA>>::type la;
+  Loader<LB, KB> lb;
   if constexpr (CONV) la.init(geo, m0, M);
   const int nk = (int)((kend - kbeg + BK - 1) / BK);
 
@@ -595,8 +608,12 @@ int64_t workspace_bytes(const comet_gemm_args& a, int splits) {
   return (int64_t)splits * a.batch[0] * a.batch[1] * a.m * a.n * (int64_t)sizeof(float);
 }
 
-template <typename T, typename TC, int LA, int LB, bool VA, bool VB>
-int launch(const comet_gemm_args& a, hipStream_t s) {
+struct LaunchCfg {
+  Epi e; Split sp; dim3 grid; int tiles_n; int splits;
+};
+
+// Epilogue flags, split count and grid shared by the bf16 and f32 launchers.
+int prepare(const comet_gemm_args& a, int bk, LaunchCfg& L) {
   const int64_t tiles_m = cdiv(a.m, BM), tiles_n = cdiv(a.n, BN);
   const int64_t nb = a.batch[0] * a.batch[1];
   COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "comet_gemm: too many tiles");
@@ -606,75 +623,145 @@ int launch(const comet_gemm_args& a, hipStream_t s) {
   };
   const int vec = a.n % 8 == 0 && v8(a.c, a.ldc, a.stride_c) && v8(a.resid, a.ldr, a.stride_r) &&
                   v8(a.aux, a.ldaux, a.stride_aux);
-  Epi e{a.bias, a.bias_mode, a.stride_bias[0], a.stride_bias[1],
-        a.resid, a.ldr, a.stride_r[0], a.stride_r[1], a.beta,
-        a.aux, a.ldaux, a.stride_aux[0], a.stride_aux[1], a.alpha, a.act, vec};
+  L.e = Epi{a.bias, a.bias_mode, a.stride_bias[0], a.stride_bias[1],
+            a.resid, a.ldr, a.stride_r[0], a.stride_r[1], a.beta,
+            a.aux, a.ldaux, a.stride_aux[0], a.stride_aux[1], a.alpha, a.act, vec};
   int splits = choose_splits(a);
-  const int bk = std::is_same<T, __bf16>::value ? bf::BK : f32::BK;
   if (splits > 1 && (a.workspace == nullptr || a.workspace_bytes < workspace_bytes(a, splits))) splits = 1;
   int64_t kchunk = a.k;
   if (splits > 1) {
     kchunk = cdiv(cdiv(a.k, bk), splits) * bk;
     splits = (int)cdiv(a.k, kchunk);
   }
-  Split sp{reinterpret_cast<float*>(a.workspace), kchunk};
-  dim3 grid((unsigned)(tiles_m * tiles_n), (unsigned)nb, (unsigned)splits);
-  const T* A = reinterpret_cast<const T*>(a.a);
-  const T* B = reinterpret_cast<const T*>(a.b);
-  TC* C = reinterpret_cast<TC*>(a.c);
-  if constexpr (std::is_same<T, __bf16>::value) {
-    if (splits > 1)
-      hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, LA, LB, VA, VB, true>), grid, dim3(NT), 0, s,
-                         A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
-                         C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1], (int)tiles_n, e, sp);
-    else
-      hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, LA, LB, VA, VB, false>), grid, dim3(NT), 0, s,
-                         A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
-                         C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1], (int)tiles_n, e, sp);
-  } else {
-    if (splits > 1)
-      hipLaunchKernelGGL((f32::gemm_f32_kernel<TC, LA, LB, VA, VB, true>), grid, dim3(NT), 0, s,
-                         A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
-                         C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1], (int)tiles_n, e, sp);
-    else
-      hipLaunchKernelGGL((f32::gemm_f32_kernel<TC, LA, LB, VA, VB, false>), grid, dim3(NT), 0, s,
-                         A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
-                         C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1], (int)tiles_n, e, sp);
-  }
-  COMET_CHECK_LAUNCH("comet_gemm");
-  if (splits > 1) {
-    const int64_t work = nb * a.m * cdiv(a.n, 4);
-    int64_t blocks = cdiv(work, 256);
-    if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL((splitk_reduce_kernel<TC>), dim3((unsigned)blocks), dim3(256), 0, s,
-                       sp.ws, splits, nb, a.batch[1], C, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, e);
-    COMET_CHECK_LAUNCH("comet_gemm split-K reduce");
-  }
+  L.sp = Split{reinterpret_cast<float*>(a.workspace), kchunk};
+  L.grid = dim3((unsigned)(tiles_m * tiles_n), (unsigned)nb, (unsigned)splits);
+  L.tiles_n = (int)tiles_n;
+  L.splits = splits;
   return COMET_OK;
 }
 
-template <typename T, typename TC, int LA, int LB>
-int dispatch_vec(const comet_gemm_args& a, hipStream_t s) {
-  constexpr int V = 16 / sizeof(T);
-  // A vector needs 16-byte alignment of every vector start: base, ld and strides multiples of V.
-  auto aligned = [&](const void* p, int64_t ld, const int64_t* st, int64_t contig_extent) {
-    return ((uintptr_t)p % 16 == 0) && ld % V == 0 && st[0] % V == 0 && st[1] % V == 0 &&
-           contig_extent % V == 0;
-  };
-  const bool va = aligned(a.a, a.lda, a.stride_a, LA == 0 ? a.k : a.m);
-  const bool vb = aligned(a.b, a.ldb, a.stride_b, LB == 0 ? a.k : a.n);
-  if (va && vb) return launch<T, TC, LA, LB, true, true>(a, s);
-  if (va) return launch<T, TC, LA, LB, true, false>(a, s);
-  if (vb) return launch<T, TC, LA, LB, false, true>(a, s);
-  return launch<T, TC, LA, LB, false, false>(a, s);
+template <typename TC>
+int reduce_splits(const comet_gemm_args& a, const LaunchCfg& L, hipStream_t s) {
+  const int64_t nb = a.batch[0] * a.batch[1];
+  const int64_t work = nb * a.m * cdiv(a.n, 4);
+  int64_t blocks = cdiv(work, 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL((splitk_reduce_kernel<TC>), dim3((unsigned)blocks), dim3(256), 0, s,
+                     L.sp.ws, L.splits, nb, a.batch[1], reinterpret_cast<TC*>(a.c), a.ldc, a.stride_c[0],
+                     a.stride_c[1], a.m, a.n, L.e);
+  COMET_CHECK_LAUNCH("comet_gemm split-K reduce");
+  return COMET_OK;
+}
+
+template <typename TC, int LA, int LB, int KA, int KB>
+int launch_bf16(const comet_gemm_args& a, hipStream_t s) {
+  LaunchCfg L;
+  int rc = prepare(a, bf::BK, L);
+  if (rc != COMET_OK) return rc;
+  // split partials are f32 whatever the output type (tiny dW GEMMs like Linear(1, 32) over all
+  // tokens have ragged operands and need the split most)
+  constexpr bool can_split = true;
+  if (!can_split && L.splits > 1) {
+    L.splits = 1;
+    L.sp.kchunk = a.k;
+    L.grid.z = 1;
+  }
+  if constexpr (can_split) {
+    if (L.splits > 1) {
+      hipLaunchKernelGGL((bf::gemm_bf16_kernel<float, LA, LB, KA, KB, true>), L.grid, dim3(NT), 0, s,
+                         a.a, a.lda, a.stride_a[0], a.stride_a[1], a.b, a.ldb, a.stride_b[0], a.stride_b[1],
+                         (float*)nullptr, a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1],
+                         L.tiles_n, L.e, L.sp);
+      COMET_CHECK_LAUNCH("comet_gemm");
+      return reduce_splits<TC>(a, L, s);
+    }
+  }
+  hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, LA, LB, KA, KB, false>), L.grid, dim3(NT), 0, s,
+                     a.a, a.lda, a.stride_a[0], a.stride_a[1], a.b, a.ldb, a.stride_b[0], a.stride_b[1],
+                     reinterpret_cast<TC*>(a.c), a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1],
+                     L.tiles_n, L.e, L.sp);
+  COMET_CHECK_LAUNCH("comet_gemm");
+  return COMET_OK;
+}
+
+template <typename TC, int LA, int LB, bool VA, bool VB>
+int launch_f32(const comet_gemm_args& a, hipStream_t s) {
+  LaunchCfg L;
+  int rc = prepare(a, f32::BK, L);
+  if (rc != COMET_OK) return rc;
+  const float* A = reinterpret_cast<const float*>(a.a);
+  const float* B = reinterpret_cast<const float*>(a.b);
+  if (L.splits > 1) {
+    hipLaunchKernelGGL((f32::gemm_f32_kernel<TC, LA, LB, VA, VB, true>), L.grid, dim3(NT), 0, s,
+                       A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
+                       reinterpret_cast<TC*>(a.c), a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1],
+                       L.tiles_n, L.e, L.sp);
+    COMET_CHECK_LAUNCH("comet_gemm");
+    return reduce_splits<TC>(a, L, s);
+  }
+  hipLaunchKernelGGL((f32::gemm_f32_kernel<TC, LA, LB, VA, VB, false>), L.grid, dim3(NT), 0, s,
+                     A, a.lda, a.stride_a[0], a.stride_a[1], B, a.ldb, a.stride_b[0], a.stride_b[1],
+                     reinterpret_cast<TC*>(a.c), a.ldc, a.stride_c[0], a.stride_c[1], a.m, a.n, a.k, a.batch[1],
+                     L.tiles_n, L.e, L.sp);
+  COMET_CHECK_LAUNCH("comet_gemm");
+  return COMET_OK;
+}
+
+// 16-B vector access: base, ld and batch strides multiples of 8 elements (bf16 or converted f32,
+// whose 8-element runs are read as 2 x 16 B) or 4 (f32 kernel), contiguous extent likewise.
+inline bool vec_ok(const void* p, int64_t ld, const int64_t* st, int64_t contig_extent, int V) {
+  return ((uintptr_t)p % 16 == 0) && ld % V == 0 && st[0] % V == 0 && st[1] % V == 0 && contig_extent % V == 0;
+}
+
+template <typename TC, int LA, int LB, int KA>
+int dispatch_kb(const comet_gemm_args& a, hipStream_t s) {
+  const bool vb = vec_ok(a.b, a.ldb, a.stride_b, LB == 0 ? a.k : a.n, 8);
+  if (a.convert_b) {
+    if constexpr (LB == 1) {
+      COMET_CHECK_ARG(vb, "comet_gemm: convert_b needs 16-B aligned f32 B with ld, strides and n multiples of 8");
+      return launch_bf16<TC, LA, LB, KA, bf::K_F32_CVT>(a, s);
+    }
+    set_error("comet_gemm: convert_b is supported for layout_b == 1 only");
+    return COMET_EINVAL;
+  }
+  if (vb) return launch_bf16<TC, LA, LB, KA, bf::K_BF16_VEC>(a, s);
+  return launch_bf16<TC, LA, LB, KA, bf::K_BF16_SCALAR>(a, s);
+}
+
+template <typename TC, int LA, int LB>
+int dispatch_bf16(const comet_gemm_args& a, hipStream_t s) {
+  const bool va = vec_ok(a.a, a.lda, a.stride_a, LA == 0 ? a.k : a.m, 8);
+  if (a.convert_a) {
+    COMET_CHECK_ARG(va, "comet_gemm: convert_a needs 16-B aligned f32 A with ld, strides and contiguous extent multiples of 8");
+    return dispatch_kb<TC, LA, LB, bf::K_F32_CVT>(a, s);
+  }
+  if (va) return dispatch_kb<TC, LA, LB, bf::K_BF16_VEC>(a, s);
+  return dispatch_kb<TC, LA, LB, bf::K_BF16_SCALAR>(a, s);
+}
+
+template <typename TC, int LA, int LB>
+int dispatch_f32(const comet_gemm_args& a, hipStream_t s) {
+  const bool va = vec_ok(a.a, a.lda, a.stride_a, LA == 0 ? a.k : a.m, 4);
+  const bool vb = vec_ok(a.b, a.ldb, a.stride_b, LB == 0 ? a.k : a.n, 4);
+  if (va && vb) return launch_f32<TC, LA, LB, true, true>(a, s);
+  if (va) return launch_f32<TC, LA, LB, true, false>(a, s);
+  if (vb) return launch_f32<TC, LA, LB, false, true>(a, s);
+  return launch_f32<TC, LA, LB, false, false>(a, s);
 }
 
 template <typename T, typename TC>
 int dispatch_layout(const comet_gemm_args& a, hipStream_t s) {
-  if (a.layout_a == 0 && a.layout_b == 0) return dispatch_vec<T, TC, 0, 0>(a, s);
-  if (a.layout_a == 0 && a.layout_b == 1) return dispatch_vec<T, TC, 0, 1>(a, s);
-  if (a.layout_a == 1 && a.layout_b == 0) return dispatch_vec<T, TC, 1, 0>(a, s);
-  return dispatch_vec<T, TC, 1, 1>(a, s);
+  if constexpr (std::is_same<T, __bf16>::value) {
+    if (a.layout_a == 0 && a.layout_b == 0) return dispatch_bf16<TC, 0, 0>(a, s);
+    if (a.layout_a == 0 && a.layout_b == 1) return dispatch_bf16<TC, 0, 1>(a, s);
+    if (a.layout_a == 1 && a.layout_b == 0) return dispatch_bf16<TC, 1, 0>(a, s);
+    return dispatch_bf16<TC, 1, 1>(a, s);
+  } else {
+    if (a.layout_a == 0 && a.layout_b == 0) return dispatch_f32<TC, 0, 0>(a, s);
+    if (a.layout_a == 0 && a.layout_b == 1) return dispatch_f32<TC, 0, 1>(a, s);
+    if (a.layout_a == 1 && a.layout_b == 0) return dispatch_f32<TC, 1, 0>(a, s);
+    return dispatch_f32<TC, 1, 1>(a, s);
+  }
 }
 
 int validate(const comet_gemm_args* args) {
@@ -687,6 +774,10 @@ int validate(const comet_gemm_args* args) {
   COMET_CHECK_ARG(a.bias_mode >= 0 && a.bias_mode <= 2, "comet_gemm: bad bias_mode");
   COMET_CHECK_ARG(a.split_k >= 0 && a.split_k <= 256, "comet_gemm: split_k must be in [0, 256]");
   COMET_CHECK_ARG(a.workspace_bytes >= 0, "comet_gemm: negative workspace_bytes");
+  COMET_CHECK_ARG(a.convert_a == 0 || a.convert_a == 1, "comet_gemm: convert_a must be 0 or 1");
+  COMET_CHECK_ARG(a.convert_b == 0 || a.convert_b == 1, "comet_gemm: convert_b must be 0 or 1");
+  COMET_CHECK_ARG(a.dtype_ab == COMET_BF16 || (a.convert_a == 0 && a.convert_b == 0),
+                  "comet_gemm: convert_a / convert_b need dtype_ab == COMET_BF16");
   return COMET_OK;
 }
 
@@ -702,7 +793,7 @@ int launch_conv(const comet_conv_args& a, hipStream_t s) {
   bf::ConvGeo g{reinterpret_cast<const __bf16*>(a.x), (int)a.h, (int)a.w, (int)a.c, a.kw, a.stride, a.pad,
                 (int)oh, (int)ow};
   Split sp{nullptr, K};
-  hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, 0, 0, true, true, false, true>),
+  hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, 0, 0, bf::K_BF16_VEC, bf::K_BF16_VEC, false, true>),
                      dim3((unsigned)(tiles_m * tiles_n), 1, 1), dim3(NT), 0, s,
                      nullptr, 0, 0, 0, reinterpret_cast<const __bf16*>(a.weight), a.ldw, 0, 0,
                      reinterpret_cast<TC*>(a.y), a.ldy, 0, 0, M, N, K, 1, (int)tiles_n, e, sp, g);

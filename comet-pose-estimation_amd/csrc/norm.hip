@@ -124,6 +124,154 @@ ln_bwd_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const float* 
   }
 }
 
+// ---- vectorised LayerNorm (cols % 8 == 0, <= 1024, 32-B aligned rows) ------------------
+// One wave per row, lane j owns columns 8j..8j+7 (and 512 + 8j.. when NV == 2): one 16-B (bf16)
+// or 2 x 16-B (f32) access per lane per row. Forward may write a second copy of y (y2, bf16) for
+// the GEMM that consumes it while y (f32) feeds a residual; backward sums two incoming
+// gradients (dy f32/bf16 + dy2 bf16) and writes dx in f32 or bf16.
+// Chunk CH = 4 (any f32 operand: 16-B f32 accesses) or 8 (all bf16: 16-B accesses); lane j owns
+// chunks j, j + 64, ... (NK per lane): every wave-wide access is one contiguous run of the row.
+template <typename TX, typename TY, int CH, int NK>
+__global__ void __launch_bounds__(256)
+ln_fwd_vec_kernel(const TX* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                  TY* __restrict__ y, __bf16* __restrict__ y2, float* __restrict__ mean_out,
+                  float* __restrict__ rstd_out, int64_t rows, int cols, int64_t ldx, int64_t ldy,
+                  int64_t ldy2, float eps, int relu) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[NK][CH];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = (lane + 64 * k) * CH;
+    if (c0 < cols) {
+      loadn<CH>(x + row * ldx + c0, v[k]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < CH; ++e) v[k][e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < CH; ++e) s += v[k][e];
+  }
+  const float mean = wave_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = (lane + 64 * k) * CH;
+    if (c0 < cols)
+#pragma unroll
+      for (int e = 0; e < CH; ++e) { const float d = v[k][e] - mean; q += d * d; }
+  }
+  const float var = wave_sum(q) / cols;
+  const float rstd = rsqrtf(var + eps);
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
+    const int c0 = (lane + 64 * k) * CH;
+    if (c0 >= cols) continue;
+    float o[CH];
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      float t = (v[k][e] - mean) * rstd;
+      if (w) t = t * w[c0 + e];
+      if (b) t = t + b[c0 + e];
+      if (relu) t = t > 0.f ? t : 0.f;
+      o[e] = t;
+    }
+    if (y) storen<CH>(y + row * ldy + c0, o);
+    if (y2) storen<CH>(y2 + row * ldy2 + c0, o);
+  }
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+template <typename TX, typename TD, typename TO, int CH, int NK>
+__global__ void __launch_bounds__(256)
+ln_bwd_vec_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const __bf16* __restrict__ dy2,
+                  const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w,
+                  TO* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db, int64_t rows, int cols,
+                  int accum) {
+  __shared__ float red[2][4][1024];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float gw[NK][CH], gb[NK][CH], wv[NK][CH];
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const int c = (lane + 64 * k) * CH + e;
+      gw[k][e] = 0.f; gb[k][e] = 0.f;
+      wv[k][e] = (w && c < cols) ? w[c] : 1.f;
+    }
+  const int64_t rbase = ((int64_t)blockIdx.x * 4 + wid) * LN_RPW;
+  for (int rr = 0; rr < LN_RPW; ++rr) {
+    const int64_t row = rbase + rr;
+    if (row >= rows) break;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NK][CH], g[NK][CH];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (lane + 64 * k) * CH;
+      if (c0 < cols) {
+        float xv[CH], d[CH];
+        loadn<CH>(x + row * cols + c0, xv);
+        loadn<CH>(dy + row * cols + c0, d);
+        if (dy2) {
+          float d2[CH];
+          loadn<CH>(dy2 + row * cols + c0, d2);
+#pragma unroll
+          for (int e = 0; e < CH; ++e) d[e] += d2[e];
+        }
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+          xh[k][e] = (xv[e] - mu) * rs;
+          gw[k][e] += d[e] * xh[k][e];
+          gb[k][e] += d[e];
+          g[k][e] = d[e] * wv[k][e];
+          s1 += g[k][e];
+          s2 += g[k][e] * xh[k][e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) { xh[k][e] = 0.f; g[k][e] = 0.f; }
+      }
+    }
+    s1 = wave_sum(s1) / cols;
+    s2 = wave_sum(s2) / cols;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (lane + 64 * k) * CH;
+      if (c0 >= cols) continue;
+      float o[CH];
+#pragma unroll
+      for (int e = 0; e < CH; ++e) o[e] = rs * (g[k][e] - s1 - xh[k][e] * s2);
+      TO* p = dx + row * cols + c0;
+      if (accum) {
+        float prev[CH];
+        loadn<CH>(p, prev);
+#pragma unroll
+        for (int e = 0; e < CH; ++e) o[e] += prev[e];
+      }
+      storen<CH>(p, o);
+    }
+  }
+  if (!dw && !db) return;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const int c = (lane + 64 * k) * CH + e;
+      if (c < cols) { red[0][wid][c] = gw[k][e]; red[1][wid][c] = gb[k][e]; }
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    if (dw) atomicAdd(dw + c, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
+    if (db) atomicAdd(db + c, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+  }
+}
+
 // InstanceNorm over H*W per (n, c) on NHWC input; one block per (n, 64-channel slab).
 // Optional fused residual: res_norm_relu==0: y = relu?(IN(x) + res); the ResidualBlock
 // tail relu(x + y) is expressed by the caller.
@@ -316,15 +464,43 @@ inline int in_chunks(int64_t n, int64_t hw, int64_t c) {
 
 using namespace comet;
 
+static bool a32(const void* p) { return ((uintptr_t)p % 32) == 0; }
+
 extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, const float* weight,
-                                   const float* bias, void* y, float* mean, float* rstd,
-                                   int64_t rows, int64_t cols, int64_t ldx, int64_t ldy, float eps,
-                                   int relu, void* stream) {
+                                   const float* bias, void* y, void* y2, float* mean, float* rstd,
+                                   int64_t rows, int64_t cols, int64_t ldx, int64_t ldy, int64_t ldy2,
+                                   float eps, int relu, void* stream) {
   COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_fwd: cols must be in [1,1024]");
-  COMET_CHECK_ARG(x && y, "comet_layernorm_fwd: null pointer");
+  COMET_CHECK_ARG(x && (y || y2), "comet_layernorm_fwd: null pointer");
   if (rows == 0) return COMET_OK;
   dim3 grid((unsigned)cdiv(rows, 4));
   hipStream_t s = as_stream(stream);
+  const bool vec = cols % 8 == 0 && ldx % 8 == 0 && (y == nullptr || ldy % 8 == 0) && (y2 == nullptr || ldy2 % 8 == 0) &&
+                   a32(x) && a32(y) && a32(y2);
+  if (vec) {
+#define LNV(TX, TY, CH, NK)                                                                               \
+  hipLaunchKernelGGL((ln_fwd_vec_kernel<TX, TY, CH, NK>), grid, dim3(256), 0, s, (const TX*)x, weight, bias, \
+                     (TY*)y, (__bf16*)y2, mean, rstd, rows, (int)cols, ldx, ldy, ldy2, eps, relu)
+#define LNV_CH(TX, TY, CH)                                                                                 \
+  do {                                                                                                     \
+    const int nk = (int)cdiv(cols, 64 * CH);                                                               \
+    if (nk == 1) LNV(TX, TY, CH, 1); else if (nk == 2) LNV(TX, TY, CH, 2);                                 \
+    else if (nk == 3) LNV(TX, TY, CH, 3); else LNV(TX, TY, CH, 4);                                         \
+  } while (0)
+#define LNV2(TX, TY)                                                                                       \
+  do { if (sizeof(TX) == 4 || (y && sizeof(TY) == 4)) LNV_CH(TX, TY, 4); else LNV_CH(TX, TY, 8); } while (0)
+    if (dtype_x == COMET_F32 && dtype_y == COMET_F32) LNV2(float, float);
+    else if (dtype_x == COMET_F32 && dtype_y == COMET_BF16) LNV2(float, __bf16);
+    else if (dtype_x == COMET_BF16 && dtype_y == COMET_F32) LNV2(__bf16, float);
+    else if (dtype_x == COMET_BF16 && dtype_y == COMET_BF16) LNV2(__bf16, __bf16);
+    else { set_error("comet_layernorm_fwd: bad dtype"); return COMET_EINVAL; }
+#undef LNV2
+#undef LNV_CH
+#undef LNV
+    COMET_CHECK_LAUNCH("comet_layernorm_fwd");
+    return COMET_OK;
+  }
+  COMET_CHECK_ARG(y2 == nullptr, "comet_layernorm_fwd: the second output needs cols % 8 == 0 and 32-B aligned rows");
 #define LNF(TX, TY)                                                                        \
   hipLaunchKernelGGL((ln_fwd_kernel<TX, TY>), grid, dim3(256), 0, s, (const TX*)x, weight, \
                      bias, (TY*)y, mean, rstd, rows, (int)cols, ldx, ldy, eps, relu)
@@ -338,18 +514,44 @@ extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, cons
   return COMET_OK;
 }
 
-extern "C" int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy,
+extern "C" int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy, const void* dy2,
                                    const float* mean, const float* rstd, const float* weight,
-                                   float* dx, float* dweight, float* dbias, int64_t rows,
+                                   int dtype_dx, void* dx, float* dweight, float* dbias, int64_t rows,
                                    int64_t cols, int dx_accumulate, void* stream) {
   COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_bwd: cols must be in [1,1024]");
   COMET_CHECK_ARG(x && dy && mean && rstd && dx, "comet_layernorm_bwd: null pointer");
   if (rows == 0) return COMET_OK;
   dim3 grid((unsigned)cdiv(rows, 4 * LN_RPW));
   hipStream_t s = as_stream(stream);
+  const bool vec = cols % 8 == 0 && a32(x) && a32(dy) && a32(dy2) && a32(dx);
+  if (vec) {
+#define LBV(TX, TD, TO, CH, NK)                                                                           \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TX, TD, TO, CH, NK>), grid, dim3(256), 0, s, (const TX*)x, (const TD*)dy, \
+                     (const __bf16*)dy2, mean, rstd, weight, (TO*)dx, dweight, dbias, rows, (int)cols, dx_accumulate)
+#define LBV_CH(TX, TD, TO, CH)                                                                             \
+  do {                                                                                                     \
+    const int nk = (int)cdiv(cols, 64 * CH);                                                               \
+    if (nk == 1) LBV(TX, TD, TO, CH, 1); else if (nk == 2) LBV(TX, TD, TO, CH, 2);                         \
+    else if (nk == 3) LBV(TX, TD, TO, CH, 3); else LBV(TX, TD, TO, CH, 4);                                 \
+  } while (0)
+#define LBV_NV(TX, TD, TO)                                                                                 \
+  do { if (sizeof(TX) == 4 || sizeof(TD) == 4 || sizeof(TO) == 4) LBV_CH(TX, TD, TO, 4); else LBV_CH(TX, TD, TO, 8); } while (0)
+#define LBV_O(TX, TD) do { if (dtype_dx == COMET_F32) LBV_NV(TX, TD, float); else LBV_NV(TX, TD, __bf16); } while (0)
+#define LBV_D(TX) do { if (dtype_dy == COMET_F32) LBV_O(TX, float); else LBV_O(TX, __bf16); } while (0)
+    if (dtype_x == COMET_F32) LBV_D(float); else LBV_D(__bf16);
+#undef LBV_D
+#undef LBV_O
+#undef LBV_NV
+#undef LBV_CH
+#undef LBV
+    COMET_CHECK_LAUNCH("comet_layernorm_bwd");
+    return COMET_OK;
+  }
+  COMET_CHECK_ARG(dy2 == nullptr && dtype_dx == COMET_F32,
+                  "comet_layernorm_bwd: dy2 / bf16 dx need cols % 8 == 0 and 32-B aligned rows");
 #define LNB(TX, TD)                                                                           \
   hipLaunchKernelGGL((ln_bwd_kernel<TX, TD>), grid, dim3(256), 0, s, (const TX*)x, (const TD*)dy, \
-                     mean, rstd, weight, dx, dweight, dbias, rows, (int)cols, dx_accumulate)
+                     mean, rstd, weight, (float*)dx, dweight, dbias, rows, (int)cols, dx_accumulate)
   if (dtype_x == COMET_F32 && dtype_dy == COMET_F32) LNB(float, float);
   else if (dtype_x == COMET_F32 && dtype_dy == COMET_BF16) LNB(float, __bf16);
   else if (dtype_x == COMET_BF16 && dtype_dy == COMET_F32) LNB(__bf16, float);

@@ -82,24 +82,36 @@ corr_kernel(PyrTab tab, int levels, int radius, const TT* __restrict__ feats, co
   const float cx = coords[t * 2], cy = coords[t * 2 + 1];
   const int win = 2 * radius + 1, gs = 2 * radius + 4;
   float* orow = out + t * ldo + col0;
+  // dot products: LPP lanes per pixel, 16 channels each (2 x 16-B loads for bf16 maps), reduced
+  // over the LPP lanes by xor shuffles; 256 / LPP pixels per pass
+  constexpr int LPP = C / 16;
+  const int sub = threadIdx.x % LPP, pslot = threadIdx.x / LPP;
+  __syncthreads();
+  float fr[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) fr[e] = f[sub * 16 + e];
   for (int l = 0; l < levels; ++l) {
     const int H = tab.h[l], W = tab.w[l];
     const TF* fm = reinterpret_cast<const TF*>(tab.p[l]) + (b * S + s) * (int64_t)H * W * C;
     const float scl = 1.f / (float)(1 << l);
     const float xl = cx * scl, yl = cy * scl;
     const int gx0 = (int)floorf(xl) - radius - 1, gy0 = (int)floorf(yl) - radius - 1;
-    __syncthreads();
-    // dot products on the pixel grid (one wave per pixel group, lanes over channels)
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int p = wid; p < gs * gs; p += 4) {
+    __syncthreads();  // previous level's dots consumed
+    for (int p0 = 0; p0 < gs * gs; p0 += 256 / LPP) {
+      const int p = p0 + pslot;
       const int px = gx0 + p % gs, py = gy0 + p / gs;
       float acc = 0.f;
-      if (px >= 0 && px < W && py >= 0 && py < H) {
-        const TF* pix = fm + ((int64_t)py * W + px) * C;
-        for (int c = lane; c < C; c += 64) acc += f[c] * to_f32(pix[c]);
+      if (p < gs * gs && px >= 0 && px < W && py >= 0 && py < H) {
+        const TF* pix = fm + ((int64_t)py * W + px) * C + sub * 16;
+        float a[8], c8[8];
+        load8(pix, a);
+        load8(pix + 8, c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += fr[e] * a[e] + fr[8 + e] * c8[e];
       }
-      acc = wave_sum(acc);
-      if (lane == 0) dots[(p / gs) * G + (p % gs)] = acc * inv_sqrt_c;
+#pragma unroll
+      for (int o = LPP / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (sub == 0 && p < gs * gs) dots[(p / gs) * G + (p % gs)] = acc * inv_sqrt_c;
     }
     __syncthreads();
     for (int k = threadIdx.x; k < win * win; k += 256) {

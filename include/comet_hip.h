@@ -77,6 +77,8 @@ typedef struct comet_gemm_args {
   int32_t act;
   void* workspace; int64_t workspace_bytes;
   int32_t split_k;
+  int32_t convert_a, convert_b;  /* 1: that operand is f32 in memory, rounded to bf16 on load
+                                    (dtype_ab must be COMET_BF16; convert_b: layout_b 1 only) */
 } comet_gemm_args;
 
 int comet_gemm(const comet_gemm_args* args, void* stream);
@@ -115,14 +117,16 @@ int comet_conv2d_nhwc(const comet_conv_args* args, void* stream);
  * (TrajectoryEncoder LN -> ReLU, camera_predictor10.py:79-81).
  * ------------------------------------------------------------------------------------- */
 int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, const float* weight,
-                        const float* bias, void* y, float* mean, float* rstd,
-                        int64_t rows, int64_t cols, int64_t ldx, int64_t ldy, float eps,
-                        int relu, void* stream);
-/* dx (f32) = LN backward; dweight/dbias (f32) are ACCUMULATED (+=) when non-NULL.
- * dx_accumulate != 0 adds into dx instead of overwriting. */
-int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy,
+                        const float* bias, void* y, void* y2, float* mean, float* rstd,
+                        int64_t rows, int64_t cols, int64_t ldx, int64_t ldy, int64_t ldy2,
+                        float eps, int relu, void* stream);
+/* y2 (bf16, may be NULL; y may be NULL when y2 is given): a second copy of the output for the GEMM
+ * that consumes it (AttnBlock: the normed x is both the in_proj input and the residual).
+ * dx (dtype_dx) = LN backward of dy + dy2 (dy2 bf16, may be NULL); dweight/dbias (f32) are
+ * ACCUMULATED (+=) when non-NULL. dx_accumulate != 0 adds into dx instead of overwriting. */
+int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy, const void* dy2,
                         const float* mean, const float* rstd, const float* weight,
-                        float* dx, float* dweight, float* dbias, int64_t rows, int64_t cols,
+                        int dtype_dx, void* dx, float* dweight, float* dbias, int64_t rows, int64_t cols,
                         int dx_accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------------
@@ -145,6 +149,29 @@ typedef struct comet_attn_args {
 } comet_attn_args;
 
 int comet_attention_fwd(const comet_attn_args* args, void* stream);
+
+/* Fused attention backward (bf16, flash style, nothing Lq x Lk in HBM): given q/k/v, the
+ * forward output o, its lse and the incoming gradient dout, writes dq, dk, dv (bf16, any
+ * 16-B-aligned strides). delta: f32 workspace [batch, heads, lq] (receives rowsum(dout*o)).
+ * Replaces autograd through nn.MultiheadAttention's bmm-softmax-bmm. */
+typedef struct comet_attn_bwd_args {
+  int32_t dtype;      /* COMET_BF16 */
+  int32_t head_dim;   /* 32, 48, 64, 96 */
+  int64_t batch, heads, lq, lk;
+  const void* q; int64_t sq_b, sq_h, sq_l;
+  const void* k; int64_t sk_b, sk_h, sk_l;
+  const void* v; int64_t sv_b, sv_h, sv_l;
+  const void* o; int64_t so_b, so_h, so_l;
+  const void* dout; int64_t sd_b, sd_h, sd_l;
+  void* dq; int64_t sdq_b, sdq_h, sdq_l;
+  void* dk; int64_t sdk_b, sdk_h, sdk_l;
+  void* dv; int64_t sdv_b, sdv_h, sdv_l;
+  const float* lse;   /* [batch, heads, lq], natural log, from comet_attention_fwd */
+  float* delta;       /* workspace [batch, heads, lq] */
+  float scale;
+} comet_attn_bwd_args;
+
+int comet_attention_bwd(const comet_attn_bwd_args* args, void* stream);
 
 /* Attention backward helpers (materialised form, head_dim-agnostic):
  * probs[r, j] = exp(s[r, j]*scale - lse[r]); s is f32, probs has dtype_s (the compute dtype);
@@ -171,6 +198,12 @@ int comet_axpby(const float* x, float* y, float a, float b, int64_t n, void* str
 /* column sum: out[c] (+)= sum_r x[r*ld + c]  (bias gradients). */
 int comet_colsum(int dtype, const void* x, float* out, int64_t rows, int64_t cols, int64_t ld,
                  int accumulate, void* stream);
+/* Linear backward prologue in one pass (cols % 8 == 0, contiguous [rows, cols], 32-B aligned):
+ * g = dy * act'(pre) (act NONE: g = dy, pre unused); if out: out = g (dtype_out);
+ * if dbias: dbias[c] (+)= sum_r g[r, c] (of the rounded g when out is bf16). */
+int comet_act_bwd_colsum(int act, int dtype_pre, const void* pre, int dtype_dy, const void* dy,
+                         int dtype_out, void* out, float* dbias, int64_t rows, int64_t cols,
+                         int accumulate, void* stream);
 /* squared L2 norm of many tensors: out[0] += sum x_i^2  (clip_grad_norm_, train_eval_func_new_cp5.py:797) */
 int comet_sq_norm_multi(const float* const* ptrs, const int64_t* sizes, int n_tensors,
                         float* out, void* stream);

@@ -298,3 +298,109 @@ def test_resize_nhwc_vector_add(dtype):
     # f32 coordinates as ATen (align_corners lambdas in f32) vs an f64 reference
     tol = 5e-5 if dtype == torch.float32 else 1.6e-2
     _close(out.permute(0, 3, 1, 2), ref, tol, tol, f"resize nhwc add {dtype}")
+
+
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("which", ["a", "b", "ab"])
+@pytest.mark.parametrize("mnk", [(200, 136, 264), (96, 64, 6000)])
+def test_gemm_f32_operands_converted_on_load(la, lb, which, mnk):
+    """bf16 GEMM with f32 operands rounded to bf16 on load (convert_a / convert_b) equals the GEMM of
+    the pre-rounded operands exactly up to f32 accumulation order."""
+    ops = _ops()
+    M, N, K = mnk
+    A = _rand(M, K, seed=40)
+    B = _rand(N, K, seed=41)
+    ref = A.to(torch.bfloat16).double() @ B.to(torch.bfloat16).double().t()
+    Ad = (A if la == 0 else A.t().contiguous()).to(DEV)
+    Bd = (B if lb == 0 else B.t().contiguous()).to(DEV)
+    if "a" not in which:
+        Ad = Ad.to(torch.bfloat16)
+    if "b" not in which:
+        Bd = Bd.to(torch.bfloat16)
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.gemm_raw(Ad, Bd, C, m=M, n=N, k=K, layout_a=la, lda=(K if la == 0 else M), layout_b=lb,
+                 ldb=(K if lb == 0 else N), ldc=N, compute=torch.bfloat16)
+    _close(C, ref, 1e-4, 1e-4 * math.sqrt(K), f"cvt gemm la={la} lb={lb} {which} {mnk}")
+
+
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+@pytest.mark.parametrize("dtypes", [(torch.float32, torch.bfloat16), (torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32)])
+def test_act_bwd_colsum(act, dtypes):
+    ops = _ops()
+    dy_dt, out_dt = dtypes
+    rows, cols = 3001, 392
+    pre = _rand(rows, cols, seed=42).to(torch.bfloat16)
+    dy = _rand(rows, cols, seed=43).to(dy_dt)
+    p = pre.double()
+    g = {0: torch.ones_like(p), 1: None, 2: (p > 0).double(), 3: torch.sigmoid(p) * (1 - torch.sigmoid(p))}[act]
+    if act == 1:
+        cdf = 0.5 * (1 + torch.erf(p / math.sqrt(2)))
+        g = cdf + p * torch.exp(-0.5 * p * p) / math.sqrt(2 * math.pi)
+    ref = dy.double() * g
+    db = torch.full((cols,), 5.0, device=DEV)
+    out = ops.act_bwd_colsum(act, pre.to(DEV), dy.to(DEV), out_dtype=out_dt, dbias=db, accumulate=True)
+    tol = 1e-5 if out_dt == torch.float32 else 8e-3
+    _close(out, ref, tol, tol, f"act_bwd_colsum out act={act}")
+    # bf16 out: db sums the rounded values; a rounding-boundary flip moves one term by 1 bf16 ulp
+    _close(db, ref.to(out_dt).double().sum(0) + 5.0, 1e-4, 1e-3 if out_dt == torch.float32 else 8e-3,
+           f"act_bwd_colsum db act={act}")
+
+
+@pytest.mark.parametrize("D", [32, 48, 64, 96])
+@pytest.mark.parametrize("lq,lk", [(577, 577), (130, 1000), (16, 16), (200, 70)])
+def test_flash_attention_bwd(D, lq, lk):
+    """comet_attention_bwd (bf16) vs f64 autograd of softmax(q k^T s) v on the same bf16 inputs,
+    with packed-projection strides like the model's (q/k/v slices of one [B, L, 3C] buffer)."""
+    ops = _ops()
+    B, H = 2, 3
+    C = H * D
+    g = torch.Generator().manual_seed(50)
+    q = torch.randn(B, lq, C, generator=g).to(torch.bfloat16)
+    kv = torch.randn(B, lk, 2 * C, generator=g).to(torch.bfloat16)
+    do = torch.randn(B, lq, C, generator=g).to(torch.bfloat16)
+    scale = D ** -0.5
+    qd, kvd = q.to(DEV), kv.to(DEV)
+    k, v = kvd[..., :C], kvd[..., C:]
+    o, lse = ops.attention(qd, k, v, H, scale, lse=True)
+    dq = torch.empty_like(qd)
+    dkv = torch.empty_like(kvd)
+    ops.attention_bwd(qd, k, v, o, lse, do.to(DEV), H, scale, dq, dkv[..., :C], dkv[..., C:])
+    # reference
+    qr = q.double().view(B, lq, H, D).transpose(1, 2).requires_grad_(True)
+    kr = kv[..., :C].double().reshape(B, lk, H, D).transpose(1, 2).requires_grad_(True)
+    vr = kv[..., C:].double().reshape(B, lk, H, D).transpose(1, 2).requires_grad_(True)
+    p = torch.softmax(qr @ kr.transpose(-1, -2) * scale, -1)
+    out = (p @ vr)
+    out.backward(o.detach().cpu().double().view(B, lq, H, D).transpose(1, 2) * 0 + do.double().view(B, lq, H, D).transpose(1, 2))
+    ref_dq = qr.grad.transpose(1, 2).reshape(B, lq, C)
+    ref_dk = kr.grad.transpose(1, 2).reshape(B, lk, C)
+    ref_dv = vr.grad.transpose(1, 2).reshape(B, lk, C)
+    for name, got, ref in (("dq", dq, ref_dq), ("dk", dkv[..., :C], ref_dk), ("dv", dkv[..., C:], ref_dv)):
+        m = ref.abs().max().item()
+        _close(got, ref, 2e-2, 2e-2 * m, f"flash bwd {name} D={D} lq={lq} lk={lk}")
+
+
+@pytest.mark.parametrize("cols", [384, 768, 1024, 130])
+def test_layernorm_dual_output_and_two_grads(cols):
+    """Vectorised LN: f32 output + bf16 copy in one kernel; backward of dy (f32) + dy2 (bf16)
+    with dx in bf16 (cols=130 exercises the scalar fallback with one output / f32 dx)."""
+    ops = _ops()
+    rows = 517
+    x = _rand(rows, cols, seed=60, scale=2.0) + 0.7
+    dy = _rand(rows, cols, seed=61)
+    dy2 = _rand(rows, cols, seed=62).to(torch.bfloat16)
+    xr = x.double().requires_grad_(True)
+    yr = F.layer_norm(xr, (cols,), eps=1e-6)
+    vec = cols % 8 == 0
+    if vec:
+        y, y16, mean, rstd = ops.layernorm(x.to(DEV), eps=1e-6, out_dtype=torch.float32, stats=True, dual=True)
+        _close(y16, yr.detach(), 8e-3, 8e-3, "ln dual bf16 copy")
+        yr.backward(dy.double() + dy2.double())
+        dx = ops.layernorm_bwd(x.to(DEV), dy.to(DEV), mean, rstd, dy2=dy2.to(DEV), dx_dtype=torch.bfloat16)
+        _close(dx, xr.grad, 1e-2, 1e-2, "ln dx (dy + dy2, bf16 out)")
+    else:
+        y, mean, rstd = ops.layernorm(x.to(DEV), eps=1e-6, out_dtype=torch.float32, stats=True)
+        yr.backward(dy.double())
+        dx = ops.layernorm_bwd(x.to(DEV), dy.to(DEV), mean, rstd)
+        _close(dx, xr.grad, 1e-4, 1e-4, "ln dx scalar path")
+    _close(y, yr.detach(), 1e-5, 1e-5, "ln y f32")
