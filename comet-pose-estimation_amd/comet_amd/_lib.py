@@ -124,7 +124,8 @@ SIGNATURES = {
     "comet_tracker_tokens": (_INT, [_INT, c_vp, c_vp, _INT, c_vp, c_i64, _INT, c_vp, _INT, c_vp, c_i64, _INT, c_vp]),
     "comet_coords_update": (_INT, [_INT, c_vp, c_vp, c_i64, c_vp, _F, c_i64, c_i64, _INT, c_vp]),
     "comet_avgpool2_nhwc": (_INT, [_INT, c_vp, c_vp, c_i64, _INT, _INT, _INT, c_vp]),
-    "comet_patch_gather": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_i64, _INT, _INT, _INT, c_vp]),
+    "comet_patch_gather": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_i64, _INT, _INT, _INT, _INT, c_vp]),
+    "comet_images_nhwc": (_INT, [_INT, c_vp, c_vp, c_i64, _INT, _INT, _INT, _INT, _INT, c_vp]),
     "comet_refine_combine": (_INT, [c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_i64, c_vp]),
     "comet_track_score": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_i64, _INT, _INT, _INT, c_vp]),
     "comet_dino_prep": (_INT, [_INT, c_vp, c_vp, c_i64, _INT, _INT, _INT, _INT, c_i64, c_vp, c_vp, c_vp]),

@@ -494,18 +494,22 @@ def harmonic(x, freqs, append_input, diag_cov=None):
     return ops.harmonic_fwd(x, freqs, append_input, diag_cov)
 
 
-def wcast_conv(w, k_align=8):
+def wcast_conv(w, k_align=8, cin_pad=None):
     """Conv weight [Cout, Cin, kh, kw] -> GEMM operand [Cout, Kpad] in the compute dtype, column
-    order (ky, kx, ci) matching comet_im2col_nhwc, K padded with zeros to k_align (cached)."""
+    order (ky, kx, ci) matching comet_im2col_nhwc / comet_conv2d_nhwc, input channels padded with
+    zeros to cin_pad (channel-padded RGB inputs) and K to k_align (cached)."""
     dt = compute_dtype()
-    key = ("conv", w.data_ptr(), tuple(w.shape), dt)
+    cout, cin, kh, kw = w.shape
+    cp = cin_pad or cin
+    key = ("conv", w.data_ptr(), tuple(w.shape), dt, cp)
     hit = _wcache.get(key)
     if hit is not None:
         return hit
-    cout, cin, kh, kw = w.shape
-    K = cin * kh * kw
+    K = cp * kh * kw
     Kp = (K + k_align - 1) // k_align * k_align
     wm = torch.zeros(cout, Kp, device=w.device, dtype=dt)
-    wm[:, :K] = w.detach().permute(0, 2, 3, 1).reshape(cout, K).to(dt)
+    wp = torch.zeros(cout, kh, kw, cp, device=w.device, dtype=dt)
+    wp[..., :cin] = w.detach().permute(0, 2, 3, 1).to(dt)
+    wm[:, :K] = wp.reshape(cout, K)
     _wcache[key] = wm
     return wm

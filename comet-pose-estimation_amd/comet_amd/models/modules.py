@@ -89,13 +89,14 @@ def conv2d_nhwc(x, conv, stride, pad, out_dtype=None):
     """nn.Conv2d on NHWC x via im2col + MFMA GEMM. conv.weight [Cout, Cin, kh, kw]."""
     w = conv.weight
     cout, cin, kh, kw = w.shape
-    wm = F.wcast_conv(w)
+    cx = x.shape[-1]  # may exceed cin: RGB inputs zero-padded to 8 channels for the implicit GEMM
+    wm = F.wcast_conv(w, cin_pad=cx)
     if kh == 1 and kw == 1 and stride == 1 and pad == 0:
         n, h, wd, c = x.shape
         y = F.linear(x.reshape(-1, c), wm, conv.bias, out_dtype=out_dtype)
         return y.reshape(n, h, wd, cout)
     xc = x if x.dtype == wm.dtype else ops.cast(x, wm.dtype)
-    if wm.dtype == torch.bfloat16 and cin % 8 == 0:  # implicit GEMM: no im2col matrix in HBM
+    if wm.dtype == torch.bfloat16 and cx % 8 == 0:  # implicit GEMM: no im2col matrix in HBM
         return ops.conv2d_nhwc(xc, wm, kh, kw, stride, pad, bias=conv.bias, out_dtype=out_dtype or wm.dtype)
     cols, oh, ow = ops.im2col_nhwc(xc, kh, kw, stride, pad, out_dtype=wm.dtype, ldc=wm.shape[1])
     y = F.linear(cols, wm, conv.bias, out_dtype=out_dtype)

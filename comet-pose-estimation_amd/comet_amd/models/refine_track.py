@@ -20,7 +20,9 @@ def refine_track(images, fine_fnet, fine_tracker, coarse_pred, pradius=15, sradi
     """images [B, S, 3, H, W] f32, coarse_pred [B, S, N, 2] ->
     (refined [B, S, N, 2], score [B, S, N] or None, inverted score [B, S, N] or None)."""
     B, S, N, _ = coarse_pred.shape
-    patches, topleft, query = ops.patch_gather(images, coarse_pred, pradius, F.compute_dtype())
+    cdt = F.compute_dtype()
+    patches, topleft, query = ops.patch_gather(images, coarse_pred, pradius, cdt,
+                                               cpad=8 if cdt == torch.bfloat16 else 3)
     feat = fine_fnet(patches)  # [B*N*S, P, P, 32]
     P, C = feat.shape[1], feat.shape[-1]
     feat = feat.reshape(B * N, S, P, P, C)

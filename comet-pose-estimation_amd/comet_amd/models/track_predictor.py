@@ -29,9 +29,11 @@ class TrackerPredictor(nn.Module):
         x = images.reshape(B * S, C, H, W)
         if self.coarse_down_ratio > 1:
             h, w = int(H / self.coarse_down_ratio), int(W / self.coarse_down_ratio)
-            x = ops.resize_bilinear(x, h, w, nhwc=False)
         else:
             h, w = H, W
-        x = ops.cast(x.permute(0, 2, 3, 1).contiguous(), F.compute_dtype())
+        # resize + NCHW -> NHWC + cast in one pass; bf16 pads RGB to 8 channels so conv1 is an
+        # implicit GEMM (zero channels x zero weights)
+        cdt = F.compute_dtype()
+        x = ops.images_nhwc(x, h, w, cdt, cpad=8 if cdt == torch.bfloat16 else 3)
         fm = self.coarse_fnet(x, h, w)
         return fm.reshape(B, S, fm.shape[1], fm.shape[2], fm.shape[3])

@@ -540,16 +540,25 @@ def avgpool2_nhwc(x):
     return y
 
 
-def patch_gather(images, coarse, pradius, out_dtype):
+def patch_gather(images, coarse, pradius, out_dtype, cpad=3):
     B, S, _, H, W = images.shape
     N = coarse.shape[2]
     P = 2 * pradius + 1
-    patches = torch.empty(B * S * N, P, P, 3, device=images.device, dtype=out_dtype)
+    patches = torch.empty(B * S * N, P, P, cpad, device=images.device, dtype=out_dtype)
     topleft = torch.empty(B, S, N, 2, device=images.device, dtype=torch.int32)
     query = torch.empty(B * N, 2, device=images.device, dtype=torch.float32)
     _chk(L.load().comet_patch_gather(dt(patches), _p(images.contiguous()), _p(coarse.contiguous()), _p(patches),
-                                     _p(topleft), _p(query), B, S, N, H, W, pradius, stream()), "patch_gather")
+                                     _p(topleft), _p(query), B, S, N, H, W, pradius, cpad, stream()), "patch_gather")
     return patches, topleft, query
+
+
+def images_nhwc(images, oh, ow, out_dtype, cpad=3):
+    """[n, 3, H, W] f32 -> [n, oh, ow, cpad] (align_corners resize when the size changes)."""
+    n, _, H, W = images.shape
+    out = torch.empty(n, oh, ow, cpad, device=images.device, dtype=out_dtype)
+    _chk(L.load().comet_images_nhwc(dt(out), _p(images.contiguous()), _p(out), n, H, W, oh, ow, cpad, stream()),
+         "images_nhwc")
+    return out
 
 
 def refine_combine(fine, topleft, coarse, B, S, N):
@@ -635,5 +644,5 @@ def _timed(fn):
 for _name in ("layernorm", "layernorm_bwd", "cast", "act_bwd", "colsum", "act_bwd_colsum", "instnorm_nhwc", "resize_bilinear",
               "im2col_nhwc", "act_fwd", "binary", "add_rows", "rowscale", "rowscale_bwd", "sample_bilinear",
               "corr_sample", "tracker_tokens", "coords_update", "avgpool2_nhwc", "patch_gather", "refine_combine",
-              "track_score", "dino_prep", "pose_encode", "pose_decode"):
+              "track_score", "dino_prep", "pose_encode", "pose_decode", "images_nhwc"):
     globals()[_name] = _timed(globals()[_name])

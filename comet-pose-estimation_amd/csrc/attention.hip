@@ -15,6 +15,8 @@
 //  * Oᵀ = Vᵀ·Pᵀ takes P straight from the Sᵀ registers as the B operand (k order permuted
 //    consistently for both operands); the Vᵀ fragments come from a row-major V tile via
 //    ds_read_b64_tr_b16 (bf16) or plain ds_read_b32 (f32).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace comet {
@@ -235,6 +237,88 @@ attn_fwd_kernel(const T* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_
   if (LSE && hg == 0) LSE[bh * lq + q] = (m_run + log2f(l_tot)) * LN2;
 }
 
+// Short sequences (Lq, Lk <= 16: the tracker's per-track time attention over S = 16 frames,
+// blocks.py:312-321): one wave per (batch, head) instead of a 64 x 64 tile that would be 1/16
+// occupied. Sᵀ = K·Qᵀ in one 16x16 MFMA tile per 32 of d (K and Q fragments straight from
+// global), column softmax over the 4 lane groups, Oᵀ = Vᵀ·Pᵀ with v_mfma_f32_16x16x16_bf16 whose
+// k = 4g + j matches the Sᵀ accumulator layout, Vᵀ fragments via ds_read_b64_tr_b16.
+template <int D>
+__global__ void __launch_bounds__(256)
+attn_small_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_l,
+                  const __bf16* __restrict__ K, int64_t sk_b, int64_t sk_h, int64_t sk_l,
+                  const __bf16* __restrict__ V, int64_t sv_b, int64_t sv_h, int64_t sv_l,
+                  __bf16* __restrict__ O, int64_t so_b, int64_t so_h, int64_t so_l,
+                  float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2, int64_t nbh) {
+  constexpr int DA = ((D + 31) / 32) * 32, NQC = DA / 32, DT = D / 16, KP = D + 8, NV = D / 8;
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[4][16 * KP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int64_t bh = (int64_t)blockIdx.x * 4 + w;
+  const bool valid = bh < nbh;
+  const int64_t b = valid ? bh / heads : 0, h = valid ? bh % heads : 0;
+  Q += b * sq_b + h * sq_h;
+  K += b * sk_b + h * sk_h;
+  V += b * sv_b + h * sv_h;
+  __bf16* vs = Vs[w];
+  for (int idx = lane; idx < 16 * NV; idx += 64) {
+    const int row = idx / NV, cv = (idx % NV) * 8;
+    const uint4 v = (valid && row < lk) ? *reinterpret_cast<const uint4*>(V + (int64_t)row * sv_l + cv) : uint4{0, 0, 0, 0};
+    *reinterpret_cast<uint4*>(vs + row * KP + cv) = v;
+  }
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NQC; ++c) {
+    const int d0 = 32 * c + 8 * g;
+    const bf16x8 qf = (valid && li < lq && d0 < D) ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)li * sq_l + d0) : bf16x8{};
+    const bf16x8 kf = (valid && li < lk && d0 < D) ? *reinterpret_cast<const bf16x8*>(K + (int64_t)li * sk_l + d0) : bf16x8{};
+    s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, s, 0, 0, 0);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float v = (4 * g + r) < lk ? s[r] * scale_log2 : -INFINITY;
+    s[r] = v;
+    m = fmaxf(m, v);
+  }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    s[r] = exp2f(s[r] - m);
+    l += s[r];
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const s16x4 pb = __builtin_bit_cast(s16x4, __builtin_convertvector(s, bf16x4));
+  __syncthreads();  // V tiles staged
+  const int qq = li >> 2, pp = li & 3;
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const s16x4 va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(vs + (4 * g + qq) * KP + 16 * dt + 4 * pp));
+    o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  }
+  if (!valid || li >= lq) return;
+  const float inv = 1.f / l;
+  __bf16* orow = O + b * so_b + h * so_h + (int64_t)li * so_l;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+    *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = __builtin_convertvector(o[dt] * inv, bf16x4);
+  if (LSE && g == 0) LSE[bh * lq + li] = (m + log2f(l)) * LN2;
+}
+
+template <int D>
+int launch_small(const comet_attn_args& a, hipStream_t s) {
+  const int64_t nbh = a.batch * a.heads;
+  hipLaunchKernelGGL((attn_small_kernel<D>), dim3((unsigned)cdiv(nbh, 4)), dim3(256), 0, s,
+                     (const __bf16*)a.q, a.sq_b, a.sq_h, a.sq_l, (const __bf16*)a.k, a.sk_b, a.sk_h, a.sk_l,
+                     (const __bf16*)a.v, a.sv_b, a.sv_h, a.sv_l, (__bf16*)a.o, a.so_b, a.so_h, a.so_l,
+                     a.lse, (int)a.heads, (int)a.lq, (int)a.lk, a.scale * LOG2E, nbh);
+  COMET_CHECK_LAUNCH("comet_attention_fwd (short)");
+  return COMET_OK;
+}
+
 template <typename T, int D>
 int launch_fwd(const comet_attn_args& a, hipStream_t s) {
   dim3 grid((unsigned)cdiv(a.lq, 64), (unsigned)(a.batch * a.heads));
@@ -248,6 +332,15 @@ int launch_fwd(const comet_attn_args& a, hipStream_t s) {
 
 template <typename T>
 int dispatch_d(const comet_attn_args& a, hipStream_t s) {
+  if (std::is_same<T, __bf16>::value && a.lq <= 16 && a.lk <= 16 && a.batch * a.heads < (1ll << 31) * 4) {
+    switch (a.head_dim) {
+      case 32: return launch_small<32>(a, s);
+      case 48: return launch_small<48>(a, s);
+      case 64: return launch_small<64>(a, s);
+      case 96: return launch_small<96>(a, s);
+      default: break;
+    }
+  }
   switch (a.head_dim) {
     case 32: return launch_fwd<T, 32>(a, s);
     case 48: return launch_fwd<T, 48>(a, s);
@@ -317,7 +410,8 @@ extern "C" int comet_attention_fwd(const comet_attn_args* args, void* stream) {
   const comet_attn_args& a = *args;
   COMET_CHECK_ARG(a.q && a.k && a.v && a.o, "comet_attention_fwd: null tensor");
   COMET_CHECK_ARG(a.batch > 0 && a.heads > 0 && a.lq >= 0 && a.lk > 0, "comet_attention_fwd: bad sizes");
-  COMET_CHECK_ARG(a.batch * a.heads <= 65535, "comet_attention_fwd: batch*heads > 65535");
+  COMET_CHECK_ARG(a.batch * a.heads <= 65535 || (a.lq <= 16 && a.lk <= 16 && a.dtype == COMET_BF16),
+                  "comet_attention_fwd: batch*heads > 65535");
   const int vec = a.dtype == COMET_BF16 ? 8 : 4;
   const int64_t strides[] = {a.sq_b, a.sq_h, a.sq_l, a.sk_b, a.sk_h, a.sk_l,
                              a.sv_b, a.sv_h, a.sv_l, a.so_b, a.so_h, a.so_l};

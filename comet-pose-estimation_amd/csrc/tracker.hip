@@ -211,11 +211,9 @@ __global__ void avgpool2_kernel(const T* __restrict__ x, T* __restrict__ y, int6
 template <typename TO>
 __global__ void patch_gather_kernel(const float* __restrict__ images, const float* __restrict__ coarse,
                                     TO* __restrict__ patches, int* __restrict__ topleft, float* __restrict__ query,
-                                    int64_t B, int S, int64_t N, int H, int W, int pradius) {
+                                    int64_t B, int S, int64_t N, int H, int W, int pradius, int cpad) {
   const int P = 2 * pradius + 1;
-  GRID_STRIDE(i, B * S * N * P * P * 3) {
-    const int ci = (int)(i % 3);
-    const int64_t q = i / 3;
+  GRID_STRIDE(q, B * S * N * P * P) {  // one thread per patch pixel, cpad channels (3.. zero)
     const int px = (int)(q % P), py = (int)((q / P) % P);
     const int64_t tp = q / ((int64_t)P * P);  // patch order (b*N + n)*S + s (fine-tracker layout)
     const int sp = (int)(tp % S);
@@ -228,8 +226,16 @@ __global__ void patch_gather_kernel(const float* __restrict__ images, const floa
     const int x0 = tlx < 0 ? 0 : (tlx > lim ? lim : tlx);
     const int y0 = tly < 0 ? 0 : (tly > lim ? lim : tly);
     const int64_t bs = t / N;
-    patches[i] = from_f32<TO>(images[((bs * 3 + ci) * H + (y0 + py)) * (int64_t)W + (x0 + px)]);
-    if (px == 0 && py == 0 && ci == 0) {
+    const int64_t pix = (int64_t)(y0 + py) * W + (x0 + px), plane = (int64_t)H * W;
+    const float* src = images + bs * 3 * plane + pix;
+    TO* dst = patches + q * cpad;
+    if (cpad == 8) {
+      float v[8] = {src[0], src[plane], src[2 * plane], 0.f, 0.f, 0.f, 0.f, 0.f};
+      store8(dst, v);
+    } else {
+      for (int c = 0; c < cpad; ++c) dst[c] = from_f32<TO>(c < 3 ? src[c * plane] : 0.f);
+    }
+    if (px == 0 && py == 0) {
       topleft[t * 2] = tlx;
       topleft[t * 2 + 1] = tly;
       const int s = (int)(bs % S);
@@ -238,6 +244,45 @@ __global__ void patch_gather_kernel(const float* __restrict__ images, const floa
         query[(b * N + n) * 2] = (cx - (float)ix) + (float)pradius;
         query[(b * N + n) * 2 + 1] = (cy - (float)iy) + (float)pradius;
       }
+    }
+  }
+}
+
+// NCHW RGB f32 -> channels-last [n, oh, ow, cpad] (channels 3.. zero) in the compute dtype, with the
+// align_corners bilinear resize of track_predictor.py:137 when (oh, ow) != (H, W).
+template <typename TO>
+__global__ void images_nhwc_kernel(const float* __restrict__ x, TO* __restrict__ y, int64_t n, int H, int W,
+                                   int oh, int ow, int cpad) {
+  GRID_STRIDE(q, n * oh * ow) {
+    const int ox = (int)(q % ow);
+    const int64_t t = q / ow;
+    const int oy = (int)(t % oh);
+    const int64_t ni = t / oh;
+    const float* xb = x + ni * 3 * (int64_t)H * W;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (oh == H && ow == W) {
+      for (int c = 0; c < 3; ++c) v[c] = xb[((int64_t)c * H + oy) * W + ox];
+    } else {
+      const float sy = oh > 1 ? (float)(H - 1) / (float)(oh - 1) : 0.f;
+      const float sx = ow > 1 ? (float)(W - 1) / (float)(ow - 1) : 0.f;
+      const float fy = sy * (float)oy, fx = sx * (float)ox;
+      int y0 = (int)fy, x0 = (int)fx;
+      y0 = y0 > H - 1 ? H - 1 : y0;
+      x0 = x0 > W - 1 ? W - 1 : x0;
+      const int y1 = y0 + 1 < H ? y0 + 1 : H - 1, x1 = x0 + 1 < W ? x0 + 1 : W - 1;
+      const float ly = fy - (float)y0, lx = fx - (float)x0;
+      for (int c = 0; c < 3; ++c) {
+        const float* pl = xb + (int64_t)c * H * W;
+        const float v00 = pl[(int64_t)y0 * W + x0], v01 = pl[(int64_t)y0 * W + x1];
+        const float v10 = pl[(int64_t)y1 * W + x0], v11 = pl[(int64_t)y1 * W + x1];
+        v[c] = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+      }
+    }
+    TO* dst = y + q * cpad;
+    if (cpad == 8) {
+      store8(dst, v);
+    } else {
+      for (int c = 0; c < cpad; ++c) dst[c] = from_f32<TO>(v[c]);
     }
   }
 }
@@ -440,18 +485,35 @@ extern "C" int comet_avgpool2_nhwc(int dtype, const void* x, void* y, int64_t n,
 
 extern "C" int comet_patch_gather(int dtype_out, const float* images, const float* coarse, void* patches,
                                   int* topleft, float* query, int64_t B, int S, int64_t N, int H, int W,
-                                  int pradius, void* stream) {
+                                  int pradius, int cpad, void* stream) {
   COMET_CHECK_ARG(images && coarse && patches && topleft && query, "comet_patch_gather: null pointer");
   COMET_CHECK_ARG(H >= 2 * pradius + 1 && W >= 2 * pradius + 1, "comet_patch_gather: image smaller than a patch");
+  COMET_CHECK_ARG(cpad >= 3 && cpad <= 8, "comet_patch_gather: cpad must be in [3, 8]");
+  COMET_CHECK_ARG(cpad != 8 || (uintptr_t)patches % 32 == 0, "comet_patch_gather: cpad 8 needs a 32-B aligned output");
   const int P = 2 * pradius + 1;
-  const int64_t tot = B * S * N * P * P * 3;
+  const int64_t tot = B * S * N * P * P;
   if (tot == 0) return COMET_OK;
   hipStream_t s = as_stream(stream);
   if (dtype_out == COMET_F32)
-    hipLaunchKernelGGL((patch_gather_kernel<float>), dim3(g1d(tot)), dim3(256), 0, s, images, coarse, (float*)patches, topleft, query, B, S, N, H, W, pradius);
+    hipLaunchKernelGGL((patch_gather_kernel<float>), dim3(g1d(tot)), dim3(256), 0, s, images, coarse, (float*)patches, topleft, query, B, S, N, H, W, pradius, cpad);
   else
-    hipLaunchKernelGGL((patch_gather_kernel<__bf16>), dim3(g1d(tot)), dim3(256), 0, s, images, coarse, (__bf16*)patches, topleft, query, B, S, N, H, W, pradius);
+    hipLaunchKernelGGL((patch_gather_kernel<__bf16>), dim3(g1d(tot)), dim3(256), 0, s, images, coarse, (__bf16*)patches, topleft, query, B, S, N, H, W, pradius, cpad);
   COMET_CHECK_LAUNCH("comet_patch_gather");
+  return COMET_OK;
+}
+
+extern "C" int comet_images_nhwc(int dtype_out, const float* images, void* out, int64_t n, int H, int W, int oh,
+                                 int ow, int cpad, void* stream) {
+  COMET_CHECK_ARG(images && out && n > 0 && H > 0 && W > 0 && oh > 0 && ow > 0, "comet_images_nhwc: bad args");
+  COMET_CHECK_ARG(cpad >= 3 && cpad <= 8, "comet_images_nhwc: cpad must be in [3, 8]");
+  COMET_CHECK_ARG(cpad != 8 || (uintptr_t)out % 32 == 0, "comet_images_nhwc: cpad 8 needs a 32-B aligned output");
+  hipStream_t s = as_stream(stream);
+  const int64_t tot = n * oh * ow;
+  if (dtype_out == COMET_F32)
+    hipLaunchKernelGGL((images_nhwc_kernel<float>), dim3(g1d(tot)), dim3(256), 0, s, images, (float*)out, n, H, W, oh, ow, cpad);
+  else
+    hipLaunchKernelGGL((images_nhwc_kernel<__bf16>), dim3(g1d(tot)), dim3(256), 0, s, images, (__bf16*)out, n, H, W, oh, ow, cpad);
+  COMET_CHECK_LAUNCH("comet_images_nhwc");
   return COMET_OK;
 }
 

@@ -309,11 +309,16 @@ int comet_coords_update(int dtype_delta, float* coords, const void* delta, int64
                         float scale, int64_t B, int64_t N, int S, void* stream);
 /* F.avg_pool2d(2, 2) on NHWC (CorrBlock pyramid, blocks.py:369-374) */
 int comet_avgpool2_nhwc(int dtype, const void* x, void* y, int64_t n, int H, int W, int C, void* stream);
-/* refine_track.py:74-131: patches NHWC [B*N*S, P, P, 3] in (b, n, s) order, topleft [B,S,N,2]
- * (int, unclamped), query [B*N,2] = frac(coarse[:, 0]) + pradius */
+/* refine_track.py:74-131: patches NHWC [B*N*S, P, P, cpad] in (b, n, s) order (RGB in channels
+ * 0..2, channels 3..cpad-1 zero: cpad 8 lets the first conv run as an implicit GEMM), topleft
+ * [B,S,N,2] (int, unclamped), query [B*N,2] = frac(coarse[:, 0]) + pradius */
 int comet_patch_gather(int dtype_out, const float* images, const float* coarse, void* patches,
                        int* topleft, float* query, int64_t B, int S, int64_t N, int H, int W,
-                       int pradius, void* stream);
+                       int pradius, int cpad, void* stream);
+/* track_predictor.py:117-143: RGB NCHW f32 [n,3,H,W] -> [n, oh, ow, cpad] (channels 3.. zero),
+ * align_corners bilinear resize when (oh, ow) != (H, W) (the x1/down_ratio interpolate). */
+int comet_images_nhwc(int dtype_out, const float* images, void* out, int64_t n, int H, int W, int oh,
+                      int ow, int cpad, void* stream);
 /* refined[b,s,n] = fine[(b*N+n), s] + topleft[b,s,n]; frame 0 = coarse query (refine_track.py:143-153) */
 int comet_refine_combine(const float* fine, const int* topleft, const float* coarse, float* refined,
                          int64_t B, int S, int64_t N, void* stream);

@@ -404,3 +404,20 @@ def test_layernorm_dual_output_and_two_grads(cols):
         dx = ops.layernorm_bwd(x.to(DEV), dy.to(DEV), mean, rstd)
         _close(dx, xr.grad, 1e-4, 1e-4, "ln dx scalar path")
     _close(y, yr.detach(), 1e-5, 1e-5, "ln y f32")
+
+
+@pytest.mark.parametrize("D", [32, 48, 64, 96])
+@pytest.mark.parametrize("lq,lk", [(16, 16), (5, 11), (16, 3), (1, 16), (9, 1)])
+def test_attention_short_sequences(D, lq, lk):
+    """Short-sequence path (one wave per (batch, head), Lq, Lk <= 16) incl. batch*heads not a
+    multiple of 4 and packed strides."""
+    ops = _ops()
+    B, H = 7, 3
+    C = H * D
+    qkv = _rand(B, 16, 3 * C, seed=70).to(torch.bfloat16)
+    q, k, v = qkv[:, :lq, :C], qkv[:, :lk, C:2 * C], qkv[:, :lk, 2 * C:]
+    ref, lse_ref = _attn_ref(q, k, v, H, D ** -0.5)
+    qd = qkv.to(DEV)
+    out, lse = ops.attention(qd[:, :lq, :C], qd[:, :lk, C:2 * C], qd[:, :lk, 2 * C:], H, D ** -0.5, lse=True)
+    _close(out, ref, 2e-2, 2e-2, f"short attn D={D} {lq}x{lk}")
+    _close(lse, lse_ref, 1e-2, 1e-2, "short attn lse")
