@@ -21,6 +21,7 @@
 // GEMMs: K = all tokens of the batch), blockIdx.z splits K; every split writes an f32 partial tile
 // into the caller's workspace and a second kernel sums the splits in a fixed order (deterministic)
 // and applies the epilogue.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.hpp"
@@ -585,6 +586,275 @@ splitk_reduce_kernel(const float* __restrict__ ws, int splits, int64_t nb, int64
   }
 }
 
+// ============================== skinny GEMM (N <= 64) =========================================
+// C[M, N] = epilogue(A[M, K] · B[N, K]ᵀ) for a narrow output (1x1 convs of the fine ShallowEncoder:
+// M = 16.7M pixels, N = K = 32): a 128-wide tile would waste 3/4 of every MFMA and epilogue pass.
+// Each wave keeps all of B (N x K) in registers as MFMA A fragments and streams 16 rows of A per
+// step as the B operand of Cᵀ = B·Aᵀ, so each lane ends with 4 consecutive output columns of one
+// row (8-B bf16 / 16-B f32 stores). Purely HBM-bound: A, resid and C move once.
+template <typename TC, int NT16, int KC>
+__global__ void __launch_bounds__(256)
+gemm_skinny_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
+                   TC* __restrict__ C, int64_t ldc, int64_t M, int N, int K, Epi epi) {
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  bf16x8 bf[NT16][KC];
+#pragma unroll
+  for (int nt = 0; nt < NT16; ++nt)
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int n = nt * 16 + li, k0 = 32 * c + 8 * g;
+      bf[nt][c] = (n < N && k0 < K) ? *reinterpret_cast<const bf16x8*>(B + (int64_t)n * ldb + k0) : bf16x8{};
+    }
+  float bias4[NT16][4];
+#pragma unroll
+  for (int nt = 0; nt < NT16; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nt * 16 + 4 * g + r;
+      bias4[nt][r] = (epi.bias && n < N) ? epi.bias[n] : 0.f;
+    }
+  const TC* R = reinterpret_cast<const TC*>(epi.resid);
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * 256) >> 6;
+  for (int64_t m0 = wave * 16; m0 < M; m0 += nwaves * 16) {
+    const int64_t m = m0 + li;
+    const bool mok = m < M;
+    f32x4 acc[NT16];
+#pragma unroll
+    for (int nt = 0; nt < NT16; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int k0 = 32 * c + 8 * g;
+      const bf16x8 a = (mok && k0 < K) ? *reinterpret_cast<const bf16x8*>(A + m * lda + k0) : bf16x8{};
+#pragma unroll
+      for (int nt = 0; nt < NT16; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[nt][c], a, acc[nt], 0, 0, 0);
+    }
+    if (!mok) continue;
+#pragma unroll
+    for (int nt = 0; nt < NT16; ++nt) {
+      const int n0 = nt * 16 + 4 * g;
+      if (n0 >= N) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(epi.act, epi.alpha * acc[nt][r] + bias4[nt][r]);
+      if (R) {
+        float rr[4];
+        load4(R + m * epi.ldr + n0, rr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += epi.beta * rr[r];
+      }
+      store4(C + m * ldc + n0, v);
+    }
+  }
+}
+
+// Eligible: bf16 A/B k-contiguous, 16-B aligned rows, N % 16 == 0, N <= 64, K % 8 == 0, K <= 256,
+// one batch, no aux, row-major C/resid with 8-B (bf16) / 16-B (f32) aligned 4-column groups.
+bool skinny_ok(const comet_gemm_args& a) {
+  if (a.dtype_ab != COMET_BF16 || a.layout_a != 0 || a.layout_b != 0 || a.convert_a || a.convert_b) return false;
+  if (a.batch[0] * a.batch[1] != 1 || a.aux != nullptr || (a.bias && a.bias_mode != 1)) return false;
+  if (a.n % 16 != 0 || a.n > 64 || a.k % 8 != 0 || a.k > 256 || a.m < 16384) return false;
+  const int es = a.dtype_c == COMET_F32 ? 4 : 2;
+  auto al = [](const void* p, int bytes) { return p == nullptr || (uintptr_t)p % bytes == 0; };
+  if (!al(a.a, 16) || a.lda % 8 != 0 || !al(a.b, 16) || a.ldb % 8 != 0) return false;
+  if ((uintptr_t)a.c % (4 * es) != 0 || a.ldc % 4 != 0) return false;
+  if (a.resid && ((uintptr_t)a.resid % (4 * es) != 0 || a.ldr % 4 != 0)) return false;
+  return true;
+}
+
+template <typename TC>
+int launch_skinny(const comet_gemm_args& a, hipStream_t s) {
+  Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, a.alpha, a.act, 0};
+  const int64_t tiles = cdiv(a.m, 16);
+  int64_t blocks = cdiv(tiles, 4 * 8);  // ~8 row tiles per wave
+  if (blocks > 4096) blocks = 4096;
+  const int nt = (int)(a.n / 16), kc = (int)cdiv(a.k, 32);
+#define SK(NT, KC)                                                                                          \
+  hipLaunchKernelGGL((gemm_skinny_kernel<TC, NT, KC>), dim3((unsigned)blocks), dim3(256), 0, s,            \
+                     (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, (int)a.n, (int)a.k, e)
+#define SK_K(NT) do { if (kc == 1) SK(NT, 1); else if (kc == 2) SK(NT, 2); else if (kc <= 4) SK(NT, 4); else SK(NT, 8); } while (0)
+  if (nt == 1) SK_K(1); else if (nt == 2) SK_K(2); else if (nt == 3) SK_K(3); else SK_K(4);
+#undef SK_K
+#undef SK
+  COMET_CHECK_LAUNCH("comet_gemm (skinny)");
+  return COMET_OK;
+}
+
+// ============================== 256 x 256 bf16 kernel (k-contiguous A and B) ==================
+// The forward Linear / 1x1 GEMMs of the step (M = all tokens, N = 384..3072, K = 256..3072).
+// 8 waves (2 x 4), each owning a 128 x 64 output block = 8 x 4 MFMA 16x16 tiles (128 accumulator
+// VGPRs); BK = 64, two LDS stages of A[256][64] and B[256][64] (128 KiB, one __shared__ array)
+// filled by global_load_lds (16 B per lane, no register staging). The glds of tile t+1 stay in
+// flight across the raw s_barrier of tile t (counted s_waitcnt vmcnt, never 0 in the loop).
+// LDS rows are 128 B; the 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7), applied on the
+// global source address (glds writes lane-linearly) and on the ds_read address, so the 16 rows a
+// ds_read_b128 lane group touches fall on 16 distinct bank slots.
+// Requires K % 64 == 0, 16-B aligned rows, one batch; M / N tails clamp the source row (the
+// garbage rows are never stored).
+namespace big {
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int STAGE = BM * BK;            // bf16 elements per operand per stage (32 KiB)
+constexpr int LDS_ELEMS = 4 * STAGE;      // A0 A1 B0 B1 = 128 KiB
+constexpr int CPW = 64 + 0;               // parked f32 pitch per wave (swizzled, no pad)
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void glds_tile(const __bf16* __restrict__ src, int64_t ld, int64_t r0, int64_t rmax,
+                                          int64_t k0, __bf16* __restrict__ img, int wid, int lane) {
+  // 32 chunks of 1 KiB (8 rows x 128 B); wave w issues chunks 4w .. 4w + 3
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = wid * 4 + i;
+    const int row = c * 8 + (lane >> 3), pch = lane & 7;
+    const int lch = pch ^ ((row >> 1) & 7);
+    int64_t gr = r0 + row;
+    gr = gr < rmax ? gr : rmax - 1;
+    const __bf16* g = src + gr * ld + k0 + lch * 8;
+    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(img + c * 512), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag(const __bf16* __restrict__ img, int row, int lchunk) {
+  return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((lchunk ^ ((row >> 1) & 7)) << 3));
+}
+
+template <typename TC>
+__global__ void __launch_bounds__(NT, 1)
+gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
+                TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, Epi epi) {
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[LDS_ELEMS];
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int li = lane & 15, g = lane >> 4;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)(K / BK);
+  glds_tile(A, lda, m0, M, 0, smem, wid, lane);
+  glds_tile(B, ldb, n0, N, 0, smem + 2 * STAGE, wid, lane);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      glds_tile(A, lda, m0, M, (int64_t)(kt + 1) * BK, smem + (cur ^ 1) * STAGE, wid, lane);
+      glds_tile(B, ldb, n0, N, (int64_t)(kt + 1) * BK, smem + (2 + (cur ^ 1)) * STAGE, wid, lane);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt landed, tile kt+1 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_barrier" ::: "memory");
+    const __bf16* a_img = smem + cur * STAGE;
+    const __bf16* b_img = smem + (2 + cur) * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag(b_img, wc * 64 + j * 16 + li, 4 * s + g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = frag(a_img, wr * 128 + i * 16 + li, 4 * s + g);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");  // stage cur free for the glds of tile kt+2
+  }
+
+  // ---- epilogue: each wave parks 64 x 64 f32 (half its block) in its own 16 KiB of LDS, then
+  // writes 8-column runs with the fused bias / act / aux / residual ----
+  float* park = reinterpret_cast<float*>(smem) + wid * 64 * CPW;
+  const TC* R = reinterpret_cast<const TC*>(epi.resid);
+  TC* X = reinterpret_cast<TC*>(epi.aux);
+  const int rq = g * 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + rq + r, col = j * 16 + li;
+          park[row * CPW + (col ^ ((row & 3) << 4))] = acc[h * 4 + i][j][r];
+        }
+    // lane: column group cg (8 columns), rows rb + 8q
+    const int cg = lane & 7, rb = lane >> 3;
+    const int64_t col0 = n0 + wc * 64 + cg * 8;
+    float bc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bc[e] = (epi.bias && epi.bias_mode == 1 && col0 + e < N) ? epi.bias[col0 + e] : 0.f;
+#pragma unroll 2
+    for (int q = 0; q < 8; ++q) {
+      const int rl = rb + 8 * q;
+      const int64_t row = m0 + wr * 128 + h * 64 + rl;
+      float v[8];
+      load8(park + rl * CPW + ((cg * 8) ^ ((rl & 3) << 4)), v);
+      if (row >= M || col0 >= N) continue;
+      const float br = (epi.bias && epi.bias_mode == 2) ? epi.bias[row] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = epi.alpha * v[e] + bc[e] + br;
+      if (epi.vec && col0 + 8 <= N) {
+        if (X) store8(X + row * epi.ldaux + col0, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = apply_act(epi.act, v[e]);
+        if (R) {
+          float rr[8];
+          load8(R + row * epi.ldr + col0, rr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += epi.beta * rr[e];
+        }
+        store8(C + row * ldc + col0, v);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int64_t col = col0 + e;
+          if (col >= N) break;
+          float o = v[e];
+          if (X) X[row * epi.ldaux + col] = from_f32<TC>(o);
+          o = apply_act(epi.act, o);
+          if (R) o += epi.beta * to_f32(R[row * epi.ldr + col]);
+          C[row * ldc + col] = from_f32<TC>(o);
+        }
+      }
+    }
+  }
+}
+}  // namespace big
+
+bool big_ok(const comet_gemm_args& a) {
+  if (a.dtype_ab != COMET_BF16 || a.layout_a != 0 || a.layout_b != 0 || a.convert_a || a.convert_b) return false;
+  if (a.batch[0] * a.batch[1] != 1 || a.k % 64 != 0 || a.k == 0) return false;
+  if (a.m < 4096 || a.n < 512) return false;  // enough 256 x 256 tiles to fill the chip
+  const int64_t npad = cdiv(a.n, 256) * 256;
+  if ((npad - a.n) * 100 > 15 * a.n) return false;  // > 15 % of the 256-wide column tiles wasted
+  if ((uintptr_t)a.a % 16 != 0 || (uintptr_t)a.b % 16 != 0 || a.lda % 8 != 0 || a.ldb % 8 != 0) return false;
+  if (a.split_k > 1) return false;
+  return true;
+}
+
+template <typename TC>
+int launch_big(const comet_gemm_args& a, hipStream_t s) {
+  auto v8 = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 32 == 0 && ld % 8 == 0); };
+  const int vec = a.n % 8 == 0 && v8(a.c, a.ldc) && v8(a.resid, a.ldr) && v8(a.aux, a.ldaux);
+  Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, vec};
+  const int64_t tiles_m = cdiv(a.m, big::BM), tiles_n = cdiv(a.n, big::BN);
+  COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "comet_gemm: too many tiles");
+  hipLaunchKernelGGL((big::gemm_big_kernel<TC>), dim3((unsigned)(tiles_m * tiles_n)), dim3(big::NT), 0, s,
+                     (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, a.n, a.k,
+                     (int)tiles_n, e);
+  COMET_CHECK_LAUNCH("comet_gemm (256x256)");
+  return COMET_OK;
+}
+
 // ---- host side --------------------------------------------------------------------------
 constexpr int kCUs = 256;
 
@@ -842,6 +1112,9 @@ extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   COMET_CHECK_ARG(a.a && a.b && a.c, "comet_gemm: null operand");
   if (a.m == 0 || a.n == 0) return COMET_OK;
   hipStream_t s = as_stream(stream);
+  if (skinny_ok(a)) return a.dtype_c == COMET_BF16 ? launch_skinny<__bf16>(a, s) : launch_skinny<float>(a, s);
+  if (big_ok(a) && getenv("COMET_GEMM_NO_BIG") == nullptr)
+    return a.dtype_c == COMET_BF16 ? launch_big<__bf16>(a, s) : launch_big<float>(a, s);
   if (a.dtype_ab == COMET_BF16 && a.dtype_c == COMET_BF16) return dispatch_layout<__bf16, __bf16>(a, s);
   if (a.dtype_ab == COMET_BF16 && a.dtype_c == COMET_F32) return dispatch_layout<__bf16, float>(a, s);
   if (a.dtype_ab == COMET_F32 && a.dtype_c == COMET_F32) return dispatch_layout<float, float>(a, s);

@@ -421,3 +421,44 @@ def test_attention_short_sequences(D, lq, lk):
     out, lse = ops.attention(qd[:, :lq, :C], qd[:, :lk, C:2 * C], qd[:, :lk, 2 * C:], H, D ** -0.5, lse=True)
     _close(out, ref, 2e-2, 2e-2, f"short attn D={D} {lq}x{lk}")
     _close(lse, lse_ref, 1e-2, 1e-2, "short attn lse")
+
+
+@pytest.mark.parametrize("n,k", [(32, 32), (16, 96), (64, 256), (48, 40)])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_gemm_skinny_narrow_outputs(n, k, out_dtype):
+    """Narrow-N path (M >= 16384, N <= 64): bias + ReLU + residual epilogue vs f64."""
+    ops = _ops()
+    M = 20001
+    x = _rand(M, k, seed=80).to(torch.bfloat16)
+    w = _rand(n, k, seed=81, scale=0.2).to(torch.bfloat16)
+    b = _rand(n, seed=82)
+    r = _rand(M, n, seed=83).to(out_dtype)
+    ref = F.relu(x.double() @ w.double().t() + b.double()) + 0.5 * r.double()
+    out = ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=2, resid=r.to(DEV), beta=0.5, out_dtype=out_dtype)
+    tol = 1e-4 if out_dtype == torch.float32 else 1e-2
+    _close(out, ref, tol, tol, f"skinny gemm n={n} k={k} {out_dtype}")
+
+
+@pytest.mark.parametrize("mnk", [(5000, 1100, 128), (4096, 512, 64), (8191, 768, 384), (4100, 1000, 192)])
+@pytest.mark.parametrize("epi", ["plain_f32", "gelu_aux_bf16", "bias_resid_f32"])
+def test_gemm_256_tile_path(mnk, epi):
+    """256 x 256 glds kernel (forward Linear shapes: k-contiguous bf16, K % 64 == 0, M >= 4096,
+    N >= 256) with M / N tails and every epilogue, vs f64."""
+    ops = _ops()
+    M, N, K = mnk
+    x = _rand(M, K, seed=90).to(torch.bfloat16)
+    w = _rand(N, K, seed=91, scale=0.1).to(torch.bfloat16)
+    b = _rand(N, seed=92)
+    pre = x.double() @ w.double().t()
+    if epi == "plain_f32":
+        out = ops.linear(x.to(DEV), w.to(DEV), out_dtype=torch.float32)
+        _close(out, pre, 1e-4, 1e-4 * math.sqrt(K), f"256 plain {mnk}")
+    elif epi == "gelu_aux_bf16":
+        aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        out = ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=1, aux=aux, out_dtype=torch.bfloat16)
+        _close(aux, pre + b.double(), 1e-2, 1e-2, f"256 aux {mnk}")
+        _close(out, F.gelu(pre + b.double()), 1e-2, 1e-2, f"256 gelu {mnk}")
+    else:
+        r = _rand(M, N, seed=93)
+        out = ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), resid=r.to(DEV), beta=0.5, out_dtype=torch.float32)
+        _close(out, pre + b.double() + 0.5 * r.double(), 1e-4, 1e-4 * math.sqrt(K), f"256 resid {mnk}")
