@@ -115,8 +115,19 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return t;
 }
 
+// nn.GELU() (exact erf form). erf by Abramowitz-Stegun 7.1.26, branch-free: |erf err| <= 1.5e-7
+// (GELU abs err <= 2.2e-7, below f32 rounding of the surrounding ops); the libm erff branches on
+// |x| < 1 and costs ~2.5x the instructions in a divergent wave -- it ran in every GEMM epilogue.
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = 1.0f - p * t * __expf(-z * z);
+  const float erf_v = copysignf(e, x);
+  return 0.5f * x * (1.0f + erf_v);
 }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));

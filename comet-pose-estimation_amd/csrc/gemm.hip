@@ -680,37 +680,38 @@ int launch_skinny(const comet_gemm_args& a, hipStream_t s) {
   return COMET_OK;
 }
 
-// ============================== 256 x 256 bf16 kernel (k-contiguous A and B) ==================
+// ============================== 256 x BN bf16 kernel (k-contiguous A and B) ===================
 // The forward Linear / 1x1 GEMMs of the step (M = all tokens, N = 384..3072, K = 256..3072).
-// 8 waves (2 x 4), each owning a 128 x 64 output block = 8 x 4 MFMA 16x16 tiles (128 accumulator
-// VGPRs); BK = 64, two LDS stages of A[256][64] and B[256][64] (128 KiB, one __shared__ array)
-// filled by global_load_lds (16 B per lane, no register staging). The glds of tile t+1 stay in
-// flight across the raw s_barrier of tile t (counted s_waitcnt vmcnt, never 0 in the loop).
-// LDS rows are 128 B; the 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7), applied on the
-// global source address (glds writes lane-linearly) and on the ds_read address, so the 16 rows a
-// ds_read_b128 lane group touches fall on 16 distinct bank slots.
-// Requires K % 64 == 0, 16-B aligned rows, one batch; M / N tails clamp the source row (the
-// garbage rows are never stored).
+// 8 waves; BN = 256: 2 x 4 waves of 128 x 64, BN = 128: 4 x 2 waves of 64 x 64 (MFMA 16x16x32,
+// 8 or 4 x 4 accumulator tiles). BK = 64, two LDS stages of A[256][64] and B[BN][64] in one
+// __shared__ array, filled by global_load_lds (16 B per lane, no register staging); tile t+1 is
+// in flight while tile t is multiplied, one raw s_barrier per k-tile. LDS rows are 128 B; the 16-B
+// chunk c of row r lives at chunk c ^ ((r >> 1) & 7) -- applied on the global source address (glds
+// writes lane-linearly) and on the ds_read address -- so the 16 rows a ds_read_b128 lane group
+// touches fall on 16 distinct bank slots. The k-step-1 fragments are read while the k-step-0
+// MFMAs run (sched_group_barrier). Requires K % 64 == 0, 16-B aligned rows, one batch; M / N tails
+// clamp the source row (those rows are never stored).
 namespace big {
-constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
-constexpr int STAGE = BM * BK;            // bf16 elements per operand per stage (32 KiB)
-constexpr int LDS_ELEMS = 4 * STAGE;      // A0 A1 B0 B1 = 128 KiB
-constexpr int CPW = 64 + 0;               // parked f32 pitch per wave (swizzled, no pad)
+constexpr int BM = 256, BK = 64, NT = 512;
+constexpr int ASTAGE = BM * BK;  // bf16 elements of one A stage (32 KiB)
+constexpr int CPW = 64;          // parked f32 pitch per wave (64 x 64, swizzled)
 
 typedef __attribute__((address_space(3))) void lds_void;
 
+// rows x 64 bf16 tile, chunks of 1 KiB (8 rows) spread over the 8 waves
+template <int ROWS>
 __device__ __forceinline__ void glds_tile(const __bf16* __restrict__ src, int64_t ld, int64_t r0, int64_t rmax,
                                           int64_t k0, __bf16* __restrict__ img, int wid, int lane) {
-  // 32 chunks of 1 KiB (8 rows x 128 B); wave w issues chunks 4w .. 4w + 3
+  constexpr int PER_WAVE = ROWS / 8 / 8;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = wid * 4 + i;
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int c = wid * PER_WAVE + i;
     const int row = c * 8 + (lane >> 3), pch = lane & 7;
     const int lch = pch ^ ((row >> 1) & 7);
     int64_t gr = r0 + row;
     gr = gr < rmax ? gr : rmax - 1;
-    const __bf16* g = src + gr * ld + k0 + lch * 8;
-    __builtin_amdgcn_global_load_lds((const void*)g, (lds_void*)(img + c * 512), 16, 0, 0);
+    const __bf16* gp = src + gr * ld + k0 + lch * 8;
+    __builtin_amdgcn_global_load_lds((const void*)gp, (lds_void*)(img + c * 512), 16, 0, 0);
   }
 }
 
@@ -718,65 +719,150 @@ __device__ __forceinline__ bf16x8 frag(const __bf16* __restrict__ img, int row, 
   return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((lchunk ^ ((row >> 1) & 7)) << 3));
 }
 
-template <typename TC>
+// Row-contiguous operands (layout 1: element (r, k) at src[k * ld + r]; the weight of dX = dY.W
+// and both operands of dW = dYᵀ.X): image [64 k][ROWS r]; 32-B unit u of k-row k lives at
+// u ^ f(k), f(k) = (k & 3) | ((k >> 3) & 1) << 2, so the 8 k-rows a half-wave reads with
+// ds_read_b64_tr_b16 hit 8 distinct 32-B bank groups. Requires rmax % 8 == 0.
+__device__ __forceinline__ int tswz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+template <int ROWS>
+__device__ __forceinline__ void glds_tile_t(const __bf16* __restrict__ src, int64_t ld, int64_t r0, int64_t rmax,
+                                            int64_t k0, __bf16* __restrict__ img, int wid, int lane) {
+  constexpr int CPR = ROWS / 8;           // 16-B chunks per k-row
+  constexpr int KPC = 64 / CPR;           // k-rows per 1-KiB wave chunk
+  constexpr int PER_WAVE = ROWS / 8 / 8;  // wave chunks per wave (64 x ROWS x 2 B / 1 KiB / 8)
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int c = wid * PER_WAVE + i;
+    const int krow = c * KPC + lane / CPR, pch = lane % CPR;
+    const int lch = pch ^ (tswz(krow) << 1);
+    int64_t gr = r0 + lch * 8;
+    gr = gr < rmax ? gr : rmax - 8;
+    const __bf16* gp = src + (k0 + krow) * ld + gr;
+    __builtin_amdgcn_global_load_lds((const void*)gp, (lds_void*)(img + c * 512), 16, 0, 0);
+  }
+}
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4g;
+
+// MFMA operand of rows rbase + (lane & 15), k = 32 s + 8 g + 0..7 from a transposed image
+template <int ROWS>
+__device__ __forceinline__ bf16x8 frag_t(const __bf16* __restrict__ img, int rbase, int s, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int u = rbase >> 4;
+  const int k0 = s * 32 + 8 * g + q, k1 = k0 + 4;
+  const __bf16* a0 = img + k0 * ROWS + ((u ^ tswz(k0)) << 4) + 4 * p;
+  const __bf16* a1 = img + k1 * ROWS + ((u ^ tswz(k1)) << 4) + 4 * p;
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(a0));
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4g*)(a1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <typename TC, int BN, int LA, int LB, bool SPLIT>
 __global__ void __launch_bounds__(NT, 1)
 gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
-                TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, Epi epi) {
-  __shared__ __attribute__((aligned(1024))) __bf16 smem[LDS_ELEMS];
+                TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, Epi epi,
+                Split sp) {
+  constexpr int WN = BN / 64, WM = 8 / WN;   // wave grid
+  constexpr int MI = BM / WM / 16;           // 16-row tiles per wave (8 or 4)
+  constexpr int BSTAGE = BN * BK;
+  constexpr int STAGING = 2 * ASTAGE + 2 * BSTAGE, PARKING = 8 * 64 * CPW * 2;  // bf16 elements
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[STAGING > PARKING ? STAGING : PARKING];
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
+  const int wr = wid / WN, wc = wid % WN;
   const int li = lane & 15, g = lane >> 4;
+  __bf16* const Asm = smem;
+  __bf16* const Bsm = smem + 2 * ASTAGE;
 
-  f32x4 acc[8][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (int)(K / BK);
-  glds_tile(A, lda, m0, M, 0, smem, wid, lane);
-  glds_tile(B, ldb, n0, N, 0, smem + 2 * STAGE, wid, lane);
+  int64_t kbeg = 0, kend = K;
+  if (SPLIT) {
+    kbeg = (int64_t)blockIdx.y * sp.kchunk;
+    kend = kbeg + sp.kchunk < K ? kbeg + sp.kchunk : K;
+  }
+  const int nk = (int)((kend - kbeg) / BK);
+  auto load_tiles = [&](int64_t k0, int stage) {
+    if constexpr (LA == 0) glds_tile<BM>(A, lda, m0, M, k0, Asm + stage * ASTAGE, wid, lane);
+    else glds_tile_t<BM>(A, lda, m0, M, k0, Asm + stage * ASTAGE, wid, lane);
+    if constexpr (LB == 0) glds_tile<BN>(B, ldb, n0, N, k0, Bsm + stage * BSTAGE, wid, lane);
+    else glds_tile_t<BN>(B, ldb, n0, N, k0, Bsm + stage * BSTAGE, wid, lane);
+  };
+  auto afrag = [&](const __bf16* img, int rbase, int s) {
+    if constexpr (LA == 0) return frag(img, rbase + li, 4 * s + g);
+    else return frag_t<BM>(img, rbase, s, lane);
+  };
+  auto bfrag = [&](const __bf16* img, int rbase, int s) {
+    if constexpr (LB == 0) return frag(img, rbase + li, 4 * s + g);
+    else return frag_t<BN>(img, rbase, s, lane);
+  };
+  if (nk > 0) load_tiles(kbeg, 0);
 
+  // one barrier per k-tile: it publishes tile kt (every wave drained its own glds first) and
+  // frees the other stage (every wave finished tile kt-1), which then receives tile kt+1 while
+  // tile kt is multiplied
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      glds_tile(A, lda, m0, M, (int64_t)(kt + 1) * BK, smem + (cur ^ 1) * STAGE, wid, lane);
-      glds_tile(B, ldb, n0, N, (int64_t)(kt + 1) * BK, smem + (2 + (cur ^ 1)) * STAGE, wid, lane);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt landed, tile kt+1 in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
-    const __bf16* a_img = smem + cur * STAGE;
-    const __bf16* b_img = smem + (2 + cur) * STAGE;
+    if (kt + 1 < nk) load_tiles(kbeg + (int64_t)(kt + 1) * BK, cur ^ 1);
+    const __bf16* a_img = Asm + cur * ASTAGE;
+    const __bf16* b_img = Bsm + cur * BSTAGE;
+    bf16x8 a0[MI], b0[4], a1[MI], b1[4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[8], bfr[4];
+    for (int j = 0; j < 4; ++j) b0[j] = bfrag(b_img, wc * 64 + j * 16, 0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag(b_img, wc * 64 + j * 16 + li, 4 * s + g);
+    for (int i = 0; i < MI; ++i) a0[i] = afrag(a_img, wr * (MI * 16) + i * 16, 0);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) af[i] = frag(a_img, wr * 128 + i * 16 + li, 4 * s + g);
+    for (int j = 0; j < 4; ++j) b1[j] = bfrag(b_img, wc * 64 + j * 16, 1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i) a1[i] = afrag(a_img, wr * (MI * 16) + i * 16, 1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], b0[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+    // order: the k-step-0 reads, then {1 read, 2 MFMA} for the k-step-1 reads, then the rest
+    constexpr int RD = MI * (LA ? 2 : 1) + 4 * (LB ? 2 : 1);  // ds_read instructions per k-step
+    constexpr int PAIRS = RD < 4 * MI ? RD : 4 * MI;
+    __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+#pragma unroll
+    for (int q = 0; q < PAIRS; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("s_barrier" ::: "memory");  // stage cur free for the glds of tile kt+2
+    __builtin_amdgcn_sched_group_barrier(0x100, RD - PAIRS, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8 * MI - 2 * PAIRS, 0);
   }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("s_barrier" ::: "memory");  // all fragment reads done before the LDS is reused
 
-  // ---- epilogue: each wave parks 64 x 64 f32 (half its block) in its own 16 KiB of LDS, then
+  // ---- epilogue: each wave parks 64 x 64 f32 in its own 16 KiB of LDS (MI / 4 rounds), then
   // writes 8-column runs with the fused bias / act / aux / residual ----
   float* park = reinterpret_cast<float*>(smem) + wid * 64 * CPW;
   const TC* R = reinterpret_cast<const TC*>(epi.resid);
   TC* X = reinterpret_cast<TC*>(epi.aux);
   const int rq = g * 4;
+  const int cg = lane & 7, rb = lane >> 3;
+  const int64_t col0 = n0 + wc * 64 + cg * 8;
+  float bc[8];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int e = 0; e < 8; ++e) bc[e] = (epi.bias && epi.bias_mode == 1 && col0 + e < N) ? epi.bias[col0 + e] : 0.f;
+#pragma unroll
+  for (int h = 0; h < MI / 4; ++h) {
+    if (h) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -786,19 +872,24 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
           const int row = i * 16 + rq + r, col = j * 16 + li;
           park[row * CPW + (col ^ ((row & 3) << 4))] = acc[h * 4 + i][j][r];
         }
-    // lane: column group cg (8 columns), rows rb + 8q
-    const int cg = lane & 7, rb = lane >> 3;
-    const int64_t col0 = n0 + wc * 64 + cg * 8;
-    float bc[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bc[e] = (epi.bias && epi.bias_mode == 1 && col0 + e < N) ? epi.bias[col0 + e] : 0.f;
 #pragma unroll 2
     for (int q = 0; q < 8; ++q) {
       const int rl = rb + 8 * q;
-      const int64_t row = m0 + wr * 128 + h * 64 + rl;
+      const int64_t row = m0 + wr * (MI * 16) + h * 64 + rl;
       float v[8];
       load8(park + rl * CPW + ((cg * 8) ^ ((rl & 3) << 4)), v);
       if (row >= M || col0 >= N) continue;
+      if constexpr (SPLIT) {  // raw f32 partial of split blockIdx.y; epilogue in the reduce
+        float* W = sp.ws + (int64_t)blockIdx.y * M * N + row * N + col0;
+        if (N % 8 == 0) {
+          store8(W, v);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (col0 + e < N) W[e] = v[e];
+        }
+        continue;
+      }
       const float br = (epi.bias && epi.bias_mode == 2) ? epi.bias[row] : 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = epi.alpha * v[e] + bc[e] + br;
@@ -830,29 +921,74 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
 }
 }  // namespace big
 
-bool big_ok(const comet_gemm_args& a) {
-  if (a.dtype_ab != COMET_BF16 || a.layout_a != 0 || a.layout_b != 0 || a.convert_a || a.convert_b) return false;
-  if (a.batch[0] * a.batch[1] != 1 || a.k % 64 != 0 || a.k == 0) return false;
-  if (a.m < 4096 || a.n < 512) return false;  // enough 256 x 256 tiles to fill the chip
-  const int64_t npad = cdiv(a.n, 256) * 256;
-  if ((npad - a.n) * 100 > 15 * a.n) return false;  // > 15 % of the 256-wide column tiles wasted
-  if ((uintptr_t)a.a % 16 != 0 || (uintptr_t)a.b % 16 != 0 || a.lda % 8 != 0 || a.ldb % 8 != 0) return false;
-  if (a.split_k > 1) return false;
-  return true;
+// 0: not eligible, else the column tile (256 or 128) wasting the fewest columns
+int big_bn(const comet_gemm_args& a) {
+  if (getenv("COMET_GEMM_NO_BIG") != nullptr) return 0;
+  if (a.dtype_ab != COMET_BF16 || a.convert_a || a.convert_b) return 0;
+  if (a.batch[0] * a.batch[1] != 1 || a.k % 64 != 0 || a.k == 0) return 0;
+  if ((uintptr_t)a.a % 16 != 0 || (uintptr_t)a.b % 16 != 0 || a.lda % 8 != 0 || a.ldb % 8 != 0) return 0;
+  if ((a.layout_a == 1 && a.m % 8 != 0) || (a.layout_b == 1 && a.n % 8 != 0)) return 0;
+  const bool wide = a.layout_a == 1 || a.layout_b == 1;  // transposed: dX / dW shapes
+  if (!wide && a.m < 4096) return 0;
+  if (a.m < 256 || a.n < 128) return 0;
+  const int64_t w256 = cdiv(a.n, 256) * 256 - a.n, w128 = cdiv(a.n, 128) * 128 - a.n;
+  if (a.n >= 512 && w256 * 100 <= 15 * a.n) return 256;
+  if (a.n % 256 == 0 || (a.n >= 512 && w128 * 100 <= 15 * a.n)) return 128;  // N = 384: 128 x 128 measured faster
+  return 0;
 }
 
-template <typename TC>
-int launch_big(const comet_gemm_args& a, hipStream_t s) {
+struct Plan {
+  int kind;      // 0 skinny, 1 256-row tile, 2 128 x 128 tile
+  int bn;        // kind 1
+  int splits;    // requested K splits (before the workspace check)
+};
+
+Plan make_plan(const comet_gemm_args& a);
+int64_t plan_workspace(const comet_gemm_args& a, const Plan& p) {
+  if (p.splits <= 1) return 0;
+  return (int64_t)p.splits * a.batch[0] * a.batch[1] * a.m * a.n * (int64_t)sizeof(float);
+}
+
+template <typename TC, int BN, int LA, int LB>
+int launch_big(const comet_gemm_args& a, int splits, hipStream_t s) {
   auto v8 = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 32 == 0 && ld % 8 == 0); };
   const int vec = a.n % 8 == 0 && v8(a.c, a.ldc) && v8(a.resid, a.ldr) && v8(a.aux, a.ldaux);
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, vec};
-  const int64_t tiles_m = cdiv(a.m, big::BM), tiles_n = cdiv(a.n, big::BN);
+  const int64_t tiles_m = cdiv(a.m, big::BM), tiles_n = cdiv(a.n, BN);
   COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "comet_gemm: too many tiles");
-  hipLaunchKernelGGL((big::gemm_big_kernel<TC>), dim3((unsigned)(tiles_m * tiles_n)), dim3(big::NT), 0, s,
+  int64_t kchunk = a.k;
+  if (splits > 1) {
+    kchunk = cdiv(a.k / 64, splits) * 64;
+    splits = (int)cdiv(a.k, kchunk);
+  }
+  Split sp{reinterpret_cast<float*>(a.workspace), kchunk};
+  dim3 grid((unsigned)(tiles_m * tiles_n), (unsigned)splits);
+  if (splits > 1) {
+    hipLaunchKernelGGL((big::gemm_big_kernel<float, BN, LA, LB, true>), grid, dim3(big::NT), 0, s,
+                       (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (float*)nullptr, a.ldc, a.m, a.n, a.k,
+                       (int)tiles_n, e, sp);
+    COMET_CHECK_LAUNCH("comet_gemm (256-row tile, split)");
+    const int64_t work = a.m * cdiv(a.n, 4);
+    int64_t blocks = cdiv(work, 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL((splitk_reduce_kernel<TC>), dim3((unsigned)blocks), dim3(256), 0, s, sp.ws, splits, (int64_t)1,
+                       (int64_t)1, (TC*)a.c, a.ldc, (int64_t)0, (int64_t)0, a.m, a.n, e);
+    COMET_CHECK_LAUNCH("comet_gemm split-K reduce");
+    return COMET_OK;
+  }
+  hipLaunchKernelGGL((big::gemm_big_kernel<TC, BN, LA, LB, false>), grid, dim3(big::NT), 0, s,
                      (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, a.n, a.k,
-                     (int)tiles_n, e);
-  COMET_CHECK_LAUNCH("comet_gemm (256x256)");
+                     (int)tiles_n, e, sp);
+  COMET_CHECK_LAUNCH("comet_gemm (256-row tile)");
   return COMET_OK;
+}
+
+template <typename TC, int BN>
+int launch_big_layout(const comet_gemm_args& a, int splits, hipStream_t s) {
+  if (a.layout_a == 0 && a.layout_b == 0) return launch_big<TC, BN, 0, 0>(a, splits, s);
+  if (a.layout_a == 0 && a.layout_b == 1) return launch_big<TC, BN, 0, 1>(a, splits, s);
+  if (a.layout_a == 1 && a.layout_b == 0) return launch_big<TC, BN, 1, 0>(a, splits, s);
+  return launch_big<TC, BN, 1, 1>(a, splits, s);
 }
 
 // ---- host side --------------------------------------------------------------------------
@@ -871,6 +1007,26 @@ int choose_splits(const comet_gemm_args& a) {
   if (s > smax) s = smax;
   if (s > 64) s = 64;
   return s < 1 ? 1 : (int)s;
+}
+
+Plan make_plan(const comet_gemm_args& a) {
+  if (skinny_ok(a)) return Plan{0, 0, 1};
+  if (const int bn = big_bn(a)) {
+    int sp = 1;
+    if (a.split_k >= 1) {
+      sp = a.split_k;
+    } else {
+      const int64_t tiles = cdiv(a.m, big::BM) * cdiv(a.n, bn), ktiles = a.k / 64;
+      if (tiles < kCUs && ktiles >= 16) {
+        int64_t s2 = cdiv(2 * kCUs, tiles);
+        if (s2 > ktiles / 8) s2 = ktiles / 8;
+        if (s2 > 64) s2 = 64;
+        sp = s2 < 1 ? 1 : (int)s2;
+      }
+    }
+    return Plan{1, bn, sp};
+  }
+  return Plan{2, 0, choose_splits(a)};
 }
 
 int64_t workspace_bytes(const comet_gemm_args& a, int splits) {
@@ -1100,7 +1256,7 @@ extern "C" int comet_gemm_workspace(const comet_gemm_args* args, int64_t* bytes)
   const int rc = validate(args);
   if (rc != COMET_OK) return rc;
   COMET_CHECK_ARG(bytes != nullptr, "comet_gemm_workspace: null bytes");
-  *bytes = workspace_bytes(*args, choose_splits(*args));
+  *bytes = plan_workspace(*args, make_plan(*args));
   return COMET_OK;
 }
 
@@ -1112,9 +1268,15 @@ extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   COMET_CHECK_ARG(a.a && a.b && a.c, "comet_gemm: null operand");
   if (a.m == 0 || a.n == 0) return COMET_OK;
   hipStream_t s = as_stream(stream);
-  if (skinny_ok(a)) return a.dtype_c == COMET_BF16 ? launch_skinny<__bf16>(a, s) : launch_skinny<float>(a, s);
-  if (big_ok(a) && getenv("COMET_GEMM_NO_BIG") == nullptr)
-    return a.dtype_c == COMET_BF16 ? launch_big<__bf16>(a, s) : launch_big<float>(a, s);
+  const Plan plan = make_plan(a);
+  if (plan.kind == 0) return a.dtype_c == COMET_BF16 ? launch_skinny<__bf16>(a, s) : launch_skinny<float>(a, s);
+  if (plan.kind == 1) {
+    int sp = plan.splits;
+    if (sp > 1 && (a.workspace == nullptr || a.workspace_bytes < plan_workspace(a, plan))) sp = 1;
+    if (plan.bn == 256)
+      return a.dtype_c == COMET_BF16 ? launch_big_layout<__bf16, 256>(a, sp, s) : launch_big_layout<float, 256>(a, sp, s);
+    return a.dtype_c == COMET_BF16 ? launch_big_layout<__bf16, 128>(a, sp, s) : launch_big_layout<float, 128>(a, sp, s);
+  }
   if (a.dtype_ab == COMET_BF16 && a.dtype_c == COMET_BF16) return dispatch_layout<__bf16, __bf16>(a, s);
   if (a.dtype_ab == COMET_BF16 && a.dtype_c == COMET_F32) return dispatch_layout<__bf16, float>(a, s);
   if (a.dtype_ab == COMET_F32 && a.dtype_c == COMET_F32) return dispatch_layout<float, float>(a, s);

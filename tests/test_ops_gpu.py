@@ -439,7 +439,8 @@ def test_gemm_skinny_narrow_outputs(n, k, out_dtype):
     _close(out, ref, tol, tol, f"skinny gemm n={n} k={k} {out_dtype}")
 
 
-@pytest.mark.parametrize("mnk", [(5000, 1100, 128), (4096, 512, 64), (8191, 768, 384), (4100, 1000, 192)])
+@pytest.mark.parametrize("mnk", [(5000, 1100, 128), (4096, 512, 64), (8191, 768, 384), (4100, 1000, 192), (4500, 256, 320),
+                                 (4097, 640, 128)])
 @pytest.mark.parametrize("epi", ["plain_f32", "gelu_aux_bf16", "bias_resid_f32"])
 def test_gemm_256_tile_path(mnk, epi):
     """256 x 256 glds kernel (forward Linear shapes: k-contiguous bf16, K % 64 == 0, M >= 4096,
@@ -462,3 +463,21 @@ def test_gemm_256_tile_path(mnk, epi):
         r = _rand(M, N, seed=93)
         out = ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), resid=r.to(DEV), beta=0.5, out_dtype=torch.float32)
         _close(out, pre + b.double() + 0.5 * r.double(), 1e-4, 1e-4 * math.sqrt(K), f"256 resid {mnk}")
+
+
+@pytest.mark.parametrize("la,lb", [(0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("mnk", [(4096, 512, 128), (768, 3072, 20480), (1000, 1000, 640), (384, 1152, 8192)])
+def test_gemm_256_tile_transposed_and_split(la, lb, mnk):
+    """256-row tile kernel with row-contiguous operands (dX = dY.W, dW = dY^T.X shapes), incl. the
+    split-K partial path for long K, vs f64."""
+    ops = _ops()
+    M, N, K = mnk
+    A = _rand(M, K, seed=100).to(torch.bfloat16)
+    B = _rand(N, K, seed=101).to(torch.bfloat16)
+    ref = A.double() @ B.double().t()
+    Ad = (A if la == 0 else A.t().contiguous()).to(DEV)
+    Bd = (B if lb == 0 else B.t().contiguous()).to(DEV)
+    C = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.gemm_raw(Ad, Bd, C, m=M, n=N, k=K, layout_a=la, lda=(K if la == 0 else M), layout_b=lb,
+                 ldb=(K if lb == 0 else N), ldc=N)
+    _close(C, ref, 1e-3, 1e-3 * math.sqrt(K), f"256 la={la} lb={lb} {mnk}")
