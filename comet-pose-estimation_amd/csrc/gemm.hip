@@ -1207,6 +1207,117 @@ int validate(const comet_gemm_args* args) {
   return COMET_OK;
 }
 
+// Narrow-output implicit convolution (cout <= 64: the fine ShallowEncoder's 32-channel convs over
+// 65536 patches): the skinny-GEMM structure (weights in registers as MFMA A fragments, 16 output
+// pixels per wave step as the B operand, Cᵀ = W·Xᵀ) with the B fragment of pixel m gathered from
+// the NHWC input tap by tap (each 8-element k chunk = 8 channels of one tap, c % 8 == 0).
+template <typename TC, int NT16, int KC>
+__global__ void __launch_bounds__(256)
+conv_skinny_kernel(const __bf16* __restrict__ X, int H, int W, int Cin, int KW, int stride, int pad, int OH, int OW,
+                   const __bf16* __restrict__ Wt, int64_t ldw, TC* __restrict__ Y, int64_t ldy, int64_t M, int N,
+                   int K, Epi epi) {
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4;
+  bf16x8 wf[NT16][KC];
+#pragma unroll
+  for (int nt = 0; nt < NT16; ++nt)
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int n = nt * 16 + li, k0 = 32 * c + 8 * g;
+      wf[nt][c] = (n < N && k0 < K) ? *reinterpret_cast<const bf16x8*>(Wt + (int64_t)n * ldw + k0) : bf16x8{};
+    }
+  float bias4[NT16][4];
+#pragma unroll
+  for (int nt = 0; nt < NT16; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nt * 16 + 4 * g + r;
+      bias4[nt][r] = (epi.bias && n < N) ? epi.bias[n] : 0.f;
+    }
+  // per-lane tap decomposition of its k chunks (fixed for the whole kernel)
+  int tky[KC], tkx[KC], tci[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const int k0 = 32 * c + 8 * g;
+    const int tap = k0 / Cin;
+    tci[c] = k0 - tap * Cin;
+    tky[c] = tap / KW;
+    tkx[c] = tap - tky[c] * KW;
+  }
+  const TC* R = reinterpret_cast<const TC*>(epi.resid);
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * 256) >> 6;
+  const unsigned short* x16 = reinterpret_cast<const unsigned short*>(X);
+  for (int64_t m0 = wave * 16; m0 < M; m0 += nwaves * 16) {
+    const int64_t m = m0 + li;
+    const bool mok = m < M;
+    int iy0 = 0, ix0 = 0;
+    int64_t base = 0;
+    if (mok) {
+      const int ox = (int)(m % OW);
+      const int64_t t = m / OW;
+      const int oy = (int)(t % OH);
+      const int64_t ni = t / OH;
+      iy0 = oy * stride - pad;
+      ix0 = ox * stride - pad;
+      base = ni * H * W * Cin;
+    }
+    f32x4 acc[NT16];
+#pragma unroll
+    for (int nt = 0; nt < NT16; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const int k0 = 32 * c + 8 * g;
+      const int iy = iy0 + tky[c], ix = ix0 + tkx[c];
+      const bool ok = mok && k0 < K && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      const bf16x8 xf = ok ? *reinterpret_cast<const bf16x8*>(x16 + base + ((int64_t)iy * W + ix) * Cin + tci[c])
+                           : bf16x8{};
+#pragma unroll
+      for (int nt = 0; nt < NT16; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt][c], xf, acc[nt], 0, 0, 0);
+    }
+    if (!mok) continue;
+#pragma unroll
+    for (int nt = 0; nt < NT16; ++nt) {
+      const int n0 = nt * 16 + 4 * g;
+      if (n0 >= N) continue;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = apply_act(epi.act, acc[nt][r] + bias4[nt][r]);
+      if (R) {
+        float rr[4];
+        load4(R + m * epi.ldr + n0, rr);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += epi.beta * rr[r];
+      }
+      store4(Y + m * ldy + n0, v);
+    }
+  }
+}
+
+template <typename TC>
+int launch_conv_skinny(const comet_conv_args& a, int64_t M, int OH, int OW, int K, hipStream_t s) {
+  Epi e{a.bias, a.bias ? 1 : 0, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, 1.f, a.act, 0};
+  int64_t blocks = cdiv(cdiv(M, 16), 4 * 8);
+  if (blocks > 4096) blocks = 4096;
+  const int nt = (int)(a.cout / 16), kc = (int)cdiv(K, 32);
+#define CSK(NT, KC)                                                                                        \
+  hipLaunchKernelGGL((conv_skinny_kernel<TC, NT, KC>), dim3((unsigned)blocks), dim3(256), 0, s,           \
+                     (const __bf16*)a.x, (int)a.h, (int)a.w, (int)a.c, a.kw, a.stride, a.pad, OH, OW,      \
+                     (const __bf16*)a.weight, a.ldw, (TC*)a.y, a.ldy, M, (int)a.cout, K, e)
+#define CSK_K(NT)                                                                                          \
+  do {                                                                                                     \
+    if (kc <= 1) CSK(NT, 1); else if (kc <= 2) CSK(NT, 2); else if (kc <= 3) CSK(NT, 3);                   \
+    else if (kc <= 4) CSK(NT, 4); else if (kc <= 6) CSK(NT, 6); else if (kc <= 8) CSK(NT, 8);              \
+    else if (NT <= 2 && kc <= 9) CSK(NT, 9); else if (NT <= 2 && kc <= 16) CSK(NT, 16);                     \
+  } while (0)
+  if (nt == 1) CSK_K(1); else if (nt == 2) CSK_K(2);
+  else if (nt == 3) { if (kc <= 8) CSK_K(3); }
+  else { if (kc <= 8) CSK_K(4); }
+#undef CSK_K
+#undef CSK
+  COMET_CHECK_LAUNCH("comet_conv2d_nhwc (narrow)");
+  return COMET_OK;
+}
+
 template <typename TC>
 int launch_conv(const comet_conv_args& a, hipStream_t s) {
   const int64_t oh = (a.h + 2 * a.pad - a.kh) / a.stride + 1, ow = (a.w + 2 * a.pad - a.kw) / a.stride + 1;
@@ -1218,6 +1329,12 @@ int launch_conv(const comet_conv_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias ? 1 : 0, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, 1.f, a.act, vec};
   bf::ConvGeo g{reinterpret_cast<const __bf16*>(a.x), (int)a.h, (int)a.w, (int)a.c, a.kw, a.stride, a.pad,
                 (int)oh, (int)ow};
+  // narrow outputs: weights fit the registers (cout/16 x ceil(K/32) fragments <= 32)
+  const int64_t kcs = cdiv(K, 32);
+  if (a.cout % 16 == 0 && a.cout <= 64 && (a.cout / 16) * kcs <= 32 && kcs <= 16 && M >= 16384 &&
+      (uintptr_t)a.y % (4 * sizeof(TC)) == 0 && a.ldy % 4 == 0 && getenv("COMET_CONV_NO_SKINNY") == nullptr &&
+      (a.resid == nullptr || ((uintptr_t)a.resid % (4 * sizeof(TC)) == 0 && a.ldr % 4 == 0)))
+    return launch_conv_skinny<TC>(a, M, (int)oh, (int)ow, (int)K, s);
   Split sp{nullptr, K};
   hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, 0, 0, bf::K_BF16_VEC, bf::K_BF16_VEC, false, true>),
                      dim3((unsigned)(tiles_m * tiles_n), 1, 1), dim3(NT), 0, s,

@@ -97,7 +97,10 @@ def test_gemm_splitk_epilogue_batched(dtype):
 
 
 @pytest.mark.parametrize("geo", [(3, 17, 13, 16, 40, 3, 1, 1), (2, 33, 30, 64, 96, 3, 2, 1), (2, 16, 16, 32, 32, 1, 2, 0),
-                                 (1, 12, 12, 416, 256, 3, 1, 1), (2, 20, 18, 8, 64, 7, 2, 3), (65, 9, 9, 32, 32, 3, 2, 1)])
+                                 (1, 12, 12, 416, 256, 3, 1, 1), (2, 20, 18, 8, 64, 7, 2, 3), (65, 9, 9, 32, 32, 3, 2, 1),
+                                 # narrow-output path (M >= 16384, cout <= 64)
+                                 (200, 16, 16, 32, 32, 3, 1, 1), (100, 31, 31, 8, 32, 3, 2, 1), (64, 20, 20, 16, 64, 3, 1, 1),
+                                 (300, 16, 16, 32, 32, 1, 2, 0), (70, 30, 30, 8, 48, 3, 1, 1)])
 @pytest.mark.parametrize("epi", ["bias", "bias_relu_resid"])
 def test_conv2d_nhwc_implicit_gemm(geo, epi):
     """comet_conv2d_nhwc (implicit GEMM, bf16) vs torch conv2d in f64 on the same bf16 inputs."""
