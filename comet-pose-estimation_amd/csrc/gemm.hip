@@ -758,7 +758,7 @@ __device__ __forceinline__ bf16x8 frag_t(const __bf16* __restrict__ img, int rba
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-template <typename TC, int BN, int LA, int LB, bool SPLIT>
+template <typename TC, int BN, int LA, int LB, bool SPLIT, int VAR = 0>
 __global__ void __launch_bounds__(NT, 1)
 gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                 TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, Epi epi,
@@ -807,23 +807,27 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
 
   // one barrier per k-tile: it publishes tile kt (every wave drained its own glds first) and
   // frees the other stage (every wave finished tile kt-1), which then receives tile kt+1 while
-  // tile kt is multiplied
-  for (int kt = 0; kt < nk; ++kt) {
+  // tile kt is multiplied. The body is branch-free (the last tile is peeled) so the scheduler can
+  // interleave the next tile's glds, this tile's fragment reads and the MFMAs.
+  auto body = [&](int kt, auto load_next) {
+    constexpr bool LOAD = decltype(load_next)::value;
     const int cur = kt & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_barrier" ::: "memory");
-    if (kt + 1 < nk) load_tiles(kbeg + (int64_t)(kt + 1) * BK, cur ^ 1);
     const __bf16* a_img = Asm + cur * ASTAGE;
     const __bf16* b_img = Bsm + cur * BSTAGE;
     bf16x8 a0[MI], b0[4], a1[MI], b1[4];
+    if constexpr (LOAD && VAR != 3) load_tiles(kbeg + (int64_t)(kt + 1) * BK, cur ^ 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) b0[j] = bfrag(b_img, wc * 64 + j * 16, 0);
 #pragma unroll
     for (int i = 0; i < MI; ++i) a0[i] = afrag(a_img, wr * (MI * 16) + i * 16, 0);
+    if constexpr (LOAD && VAR == 3) load_tiles(kbeg + (int64_t)(kt + 1) * BK, cur ^ 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) b1[j] = bfrag(b_img, wc * 64 + j * 16, 1);
 #pragma unroll
     for (int i = 0; i < MI; ++i) a1[i] = afrag(a_img, wr * (MI * 16) + i * 16, 1);
+    if constexpr (VAR == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -834,18 +838,37 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
-    // order: the k-step-0 reads, then {1 read, 2 MFMA} for the k-step-1 reads, then the rest
+    if constexpr (VAR == 1) __builtin_amdgcn_s_setprio(0);
     constexpr int RD = MI * (LA ? 2 : 1) + 4 * (LB ? 2 : 1);  // ds_read instructions per k-step
-    constexpr int PAIRS = RD < 4 * MI ? RD : 4 * MI;
-    __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+    if constexpr (VAR == 3) {
+      constexpr int NG = LOAD ? BM / 64 + BN / 64 : 0;       // glds per thread per tile
+      __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
 #pragma unroll
-    for (int q = 0; q < PAIRS; ++q) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      for (int q = 0; q < NG; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < RD; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8 * MI - 2 * NG - RD, 0);
+    } else if constexpr (VAR != 2) {
+      // the k-step-0 reads, then {1 read, 2 MFMA} for the k-step-1 reads, then the rest
+      constexpr int PAIRS = RD < 4 * MI ? RD : 4 * MI;
+      __builtin_amdgcn_sched_group_barrier(0x100, RD, 0);
+#pragma unroll
+      for (int q = 0; q < PAIRS; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, RD - PAIRS, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 8 * MI - 2 * PAIRS, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x100, RD - PAIRS, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 8 * MI - 2 * PAIRS, 0);
-  }
+  };
+  for (int kt = 0; kt + 1 < nk; ++kt) body(kt, std::true_type{});
+  if (nk > 0) body(nk - 1, std::false_type{});
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   asm volatile("s_barrier" ::: "memory");  // all fragment reads done before the LDS is reused
 

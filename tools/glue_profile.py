@@ -33,6 +33,8 @@ def main():
         with F.precision(torch.bfloat16):
             train_step(model, img, cams, tracks, opt, sched, cfg)
         torch.cuda.synchronize()
+    print(prof.key_averages(group_by_stack_n=6).table(sort_by="self_device_time_total", row_limit=25,
+                                                       max_name_column_width=40))
     agg = collections.defaultdict(lambda: [0, 0.0])
     for ev in prof.events():
         if not ev.name.startswith("aten::") or ev.device_time_total <= 0:
