@@ -55,6 +55,7 @@ class AttnArgs(ctypes.Structure):
         ("v", c_vp), ("sv_b", c_i64), ("sv_h", c_i64), ("sv_l", c_i64),
         ("o", c_vp), ("so_b", c_i64), ("so_h", c_i64), ("so_l", c_i64),
         ("lse", c_vp), ("scale", ctypes.c_float),
+        ("batch_inner", c_i64), ("sq_i", c_i64), ("sk_i", c_i64), ("sv_i", c_i64), ("so_i", c_i64),
     ]
 
 

@@ -123,31 +123,34 @@ class EfficientUpdateFormer(nn.Module):
 
     @torch.no_grad()
     def forward(self, input_tensor, mask=None):
-        """input [B, N, T, Din] (compute dtype) -> [B, N, T, Dout] f32."""
+        """input [B, N, T, Din] (compute dtype) -> [B, N, T, Dout] f32.
+
+        The reference concatenates the virtual tracks to the point tracks and permutes
+        [B, N, T, C] <-> [B*T, N, C] around every space block (blocks.py:300-345). Here point and
+        virtual tokens live in two [B, n, T, C] tensors: the time blocks are per-track (run on
+        each), the space blocks attend over the track axis of the 4-D tensors directly (inner-batch
+        attention over (b, t)), so no cat / permute copies are made."""
         B, N0, T, _ = input_tensor.shape
-        init = F.linear(input_tensor, self.input_transform.weight, self.input_transform.bias, out_dtype=torch.float32)
-        tokens = init
-        if self.add_space_attn:
-            vt = self.virual_tracks.detach().float().expand(B, -1, T, -1)
-            tokens = torch.cat([tokens, vt], dim=1)
-        N = tokens.shape[1]
         C = self.hidden_size
+        init = F.linear(input_tensor, self.input_transform.weight, self.input_transform.bias, out_dtype=torch.float32)
+        pts = init
+        vts = None
+        if self.add_space_attn:
+            vts = self.virual_tracks.detach().float().expand(B, -1, T, -1).contiguous()
+        Nv = self.num_virtual_tracks if self.add_space_attn else 0
         j = 0
         space_every = len(self.time_blocks) // len(self.space_virtual_blocks) if self.add_space_attn else 0
         for i in range(len(self.time_blocks)):
-            tokens = self.time_blocks[i](tokens.reshape(B * N, T, C)).reshape(B, N, T, C)
+            blk = self.time_blocks[i]
+            pts = blk(pts.reshape(B * N0, T, C)).reshape(B, N0, T, C)
+            if vts is not None:
+                vts = blk(vts.reshape(B * Nv, T, C)).reshape(B, Nv, T, C)
             if self.add_space_attn and i % space_every == 0:
-                st = tokens.permute(0, 2, 1, 3).reshape(B * T, N, C)
-                pt = st[:, :N - self.num_virtual_tracks]
-                vt = st[:, N - self.num_virtual_tracks:]
-                vt = self.space_virtual2point_blocks[j](vt, pt)
-                vt = self.space_virtual_blocks[j](vt)
-                pt = self.space_point2virtual_blocks[j](pt, vt)
-                tokens = torch.cat([pt, vt], dim=1).reshape(B, T, N, C).permute(0, 2, 1, 3).contiguous()
+                vts = self.space_virtual2point_blocks[j](vts, pts)
+                vts = self.space_virtual_blocks[j](vts)
+                pts = self.space_point2virtual_blocks[j](pts, vts)
                 j += 1
-        if self.add_space_attn:
-            tokens = tokens[:, :N - self.num_virtual_tracks]
-        return _flow(tokens, init, self.flow_head)
+        return _flow(pts, init, self.flow_head)
 
 
 def _flow(tokens, init, head):

@@ -221,31 +221,40 @@ def layernorm_bwd(x, dy, mean, rstd, weight=None, dweight=None, dbias=None, dx=N
 # ------------------------------------------------------------------------------------------
 def attention(q, k, v, heads, scale=None, out=None, lse=False):
     """Multi-head attention on token-major views: q [B, Lq, H*D], k/v [B, Lk, H*D] (last dim
-    unit-stride; rows may be strided, e.g. slices of a packed qkv projection)."""
+    unit-stride; rows may be strided, e.g. slices of a packed qkv projection). 4-D views
+    [B, L, T, H*D] attend over L for every (b, t) (inner batch, no permute)."""
     _req_cuda(q, k, v)
-    B, Lq, C = q.shape
+    inner = q.dim() == 4
+    if inner:
+        B, Lq, T, C = q.shape
+    else:
+        B, Lq, C = q.shape
+        T = 1
     Lk = k.shape[1]
     D = C // heads
-    if q.stride(2) != 1 or k.stride(2) != 1 or v.stride(2) != 1:
+    if q.stride(-1) != 1 or k.stride(-1) != 1 or v.stride(-1) != 1:
         raise L.CometHipError("attention: head dim must be unit-stride")
     if scale is None:
         scale = D ** -0.5
     if out is None:
-        out = torch.empty(B, Lq, C, device=q.device, dtype=q.dtype)
-    lse_t = torch.empty(B, heads, Lq, device=q.device, dtype=torch.float32) if lse else None
+        out = torch.empty(q.shape, device=q.device, dtype=q.dtype)
+    lse_t = torch.empty(B * T, heads, Lq, device=q.device, dtype=torch.float32) if lse else None
     a = L.AttnArgs()
     a.dtype, a.head_dim = dt(q), D
-    a.batch, a.heads, a.lq, a.lk = B, heads, Lq, Lk
+    a.batch, a.heads, a.lq, a.lk = B * T, heads, Lq, Lk
     a.q, a.sq_b, a.sq_h, a.sq_l = _p(q), q.stride(0), D, q.stride(1)
     a.k, a.sk_b, a.sk_h, a.sk_l = _p(k), k.stride(0), D, k.stride(1)
     a.v, a.sv_b, a.sv_h, a.sv_l = _p(v), v.stride(0), D, v.stride(1)
     a.o, a.so_b, a.so_h, a.so_l = _p(out), out.stride(0), D, out.stride(1)
+    if inner:
+        a.batch_inner = T
+        a.sq_i, a.sk_i, a.sv_i, a.so_i = q.stride(2), k.stride(2), v.stride(2), out.stride(2)
     a.lse, a.scale = _p(lse_t), float(scale)
     e0 = PROF.start()
     L.check(L.load().comet_attention_fwd(ctypes.byref(a), stream()), "attention")
     if e0 is not None:
-        name = f"attn fwd B{B} H{heads} Lq{Lq} Lk{Lk} D{D}" if PROF.detail else "comet_attention_fwd"
-        PROF.stop(e0, name, 4.0 * B * heads * Lq * Lk * D)
+        name = f"attn fwd B{B} T{T} H{heads} Lq{Lq} Lk{Lk} D{D}" if PROF.detail else "comet_attention_fwd"
+        PROF.stop(e0, name, 4.0 * B * T * heads * Lq * Lk * D)
     return (out, lse_t) if lse else out
 
 

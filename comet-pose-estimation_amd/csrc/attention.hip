@@ -37,6 +37,10 @@ template <int D> struct ACfg<float, D> {
   static constexpr int VEC = 4;
 };
 
+// optional inner batch: batch index b = (b / n) * s*_b + (b % n) * s*  (the tracker's space
+// attention runs over tracks of a [B, N, T, C] tensor for every (b, t) without permuting it)
+struct Inner { int64_t n, sq, sk, sv, so; };
+
 template <typename T> struct AVec;
 template <> struct AVec<__bf16> { typedef uint4 type; };
 template <> struct AVec<float> { typedef float4 type; };
@@ -49,7 +53,7 @@ attn_fwd_kernel(const T* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_
                 const T* __restrict__ K, int64_t sk_b, int64_t sk_h, int64_t sk_l,
                 const T* __restrict__ V, int64_t sv_b, int64_t sv_h, int64_t sv_l,
                 T* __restrict__ O, int64_t so_b, int64_t so_h, int64_t so_l,
-                float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2) {
+                float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2, Inner in) {
   typedef ACfg<T, D> C;
   constexpr int DA = C::DA, KP = C::KP, VEC = C::VEC;
   constexpr int DT = (D + 15) / 16;
@@ -65,10 +69,11 @@ attn_fwd_kernel(const T* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_
   const int li = lane & 15, hg = lane >> 4;
   const int64_t bh = blockIdx.y;
   const int64_t b = bh / heads, h = bh % heads;
-  Q += b * sq_b + h * sq_h;
-  K += b * sk_b + h * sk_h;
-  V += b * sv_b + h * sv_h;
-  O += b * so_b + h * so_h;
+  const int64_t bo = b / in.n, bi = b % in.n;
+  Q += bo * sq_b + bi * in.sq + h * sq_h;
+  K += bo * sk_b + bi * in.sk + h * sk_h;
+  V += bo * sv_b + bi * in.sv + h * sv_h;
+  O += bo * so_b + bi * in.so + h * so_h;
 
   // zero LDS once: pad columns [D, DA) stay zero for the whole kernel
   for (int i = tid; i < 64 * KP; i += 256) { Ks[i] = T(0.f); Vs[i] = T(0.f); }
@@ -248,7 +253,7 @@ attn_small_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
                   const __bf16* __restrict__ K, int64_t sk_b, int64_t sk_h, int64_t sk_l,
                   const __bf16* __restrict__ V, int64_t sv_b, int64_t sv_h, int64_t sv_l,
                   __bf16* __restrict__ O, int64_t so_b, int64_t so_h, int64_t so_l,
-                  float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2, int64_t nbh) {
+                  float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2, int64_t nbh, Inner in) {
   constexpr int DA = ((D + 31) / 32) * 32, NQC = DA / 32, DT = D / 16, KP = D + 8, NV = D / 8;
   __shared__ __attribute__((aligned(16))) __bf16 Vs[4][16 * KP];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -256,9 +261,10 @@ attn_small_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
   const int64_t bh = (int64_t)blockIdx.x * 4 + w;
   const bool valid = bh < nbh;
   const int64_t b = valid ? bh / heads : 0, h = valid ? bh % heads : 0;
-  Q += b * sq_b + h * sq_h;
-  K += b * sk_b + h * sk_h;
-  V += b * sv_b + h * sv_h;
+  const int64_t bo = b / in.n, bi = b % in.n;
+  Q += bo * sq_b + bi * in.sq + h * sq_h;
+  K += bo * sk_b + bi * in.sk + h * sk_h;
+  V += bo * sv_b + bi * in.sv + h * sv_h;
   __bf16* vs = Vs[w];
   for (int idx = lane; idx < 16 * NV; idx += 64) {
     const int row = idx / NV, cv = (idx % NV) * 8;
@@ -301,11 +307,16 @@ attn_small_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
   }
   if (!valid || li >= lq) return;
   const float inv = 1.f / l;
-  __bf16* orow = O + b * so_b + h * so_h + (int64_t)li * so_l;
+  __bf16* orow = O + bo * so_b + bi * in.so + h * so_h + (int64_t)li * so_l;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
     *reinterpret_cast<bf16x4*>(orow + 16 * dt + 4 * g) = __builtin_convertvector(o[dt] * inv, bf16x4);
   if (LSE && g == 0) LSE[bh * lq + li] = (m + log2f(l)) * LN2;
+}
+
+inline Inner inner_of(const comet_attn_args& a) {
+  if (a.batch_inner <= 1) return Inner{1, 0, 0, 0, 0};
+  return Inner{a.batch_inner, a.sq_i, a.sk_i, a.sv_i, a.so_i};
 }
 
 template <int D>
@@ -314,7 +325,7 @@ int launch_small(const comet_attn_args& a, hipStream_t s) {
   hipLaunchKernelGGL((attn_small_kernel<D>), dim3((unsigned)cdiv(nbh, 4)), dim3(256), 0, s,
                      (const __bf16*)a.q, a.sq_b, a.sq_h, a.sq_l, (const __bf16*)a.k, a.sk_b, a.sk_h, a.sk_l,
                      (const __bf16*)a.v, a.sv_b, a.sv_h, a.sv_l, (__bf16*)a.o, a.so_b, a.so_h, a.so_l,
-                     a.lse, (int)a.heads, (int)a.lq, (int)a.lk, a.scale * LOG2E, nbh);
+                     a.lse, (int)a.heads, (int)a.lq, (int)a.lk, a.scale * LOG2E, nbh, inner_of(a));
   COMET_CHECK_LAUNCH("comet_attention_fwd (short)");
   return COMET_OK;
 }
@@ -325,7 +336,7 @@ int launch_fwd(const comet_attn_args& a, hipStream_t s) {
   hipLaunchKernelGGL((attn_fwd_kernel<T, D>), grid, dim3(256), 0, s,
                      (const T*)a.q, a.sq_b, a.sq_h, a.sq_l, (const T*)a.k, a.sk_b, a.sk_h, a.sk_l,
                      (const T*)a.v, a.sv_b, a.sv_h, a.sv_l, (T*)a.o, a.so_b, a.so_h, a.so_l,
-                     a.lse, (int)a.heads, (int)a.lq, (int)a.lk, a.scale * LOG2E);
+                     a.lse, (int)a.heads, (int)a.lq, (int)a.lk, a.scale * LOG2E, inner_of(a));
   COMET_CHECK_LAUNCH("comet_attention_fwd");
   return COMET_OK;
 }
@@ -413,8 +424,10 @@ extern "C" int comet_attention_fwd(const comet_attn_args* args, void* stream) {
   COMET_CHECK_ARG(a.batch * a.heads <= 65535 || (a.lq <= 16 && a.lk <= 16 && a.dtype == COMET_BF16),
                   "comet_attention_fwd: batch*heads > 65535");
   const int vec = a.dtype == COMET_BF16 ? 8 : 4;
+  COMET_CHECK_ARG(a.batch_inner >= 0 && (a.batch_inner <= 1 || a.batch % a.batch_inner == 0),
+                  "comet_attention_fwd: batch must be a multiple of batch_inner");
   const int64_t strides[] = {a.sq_b, a.sq_h, a.sq_l, a.sk_b, a.sk_h, a.sk_l,
-                             a.sv_b, a.sv_h, a.sv_l, a.so_b, a.so_h, a.so_l};
+                             a.sv_b, a.sv_h, a.sv_l, a.so_b, a.so_h, a.so_l, a.sq_i, a.sk_i, a.sv_i, a.so_i};
   for (int64_t st : strides) COMET_CHECK_ARG(st % vec == 0, "comet_attention_fwd: strides must be multiples of 16 bytes");
   COMET_CHECK_ARG(((uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v | (uintptr_t)a.o) % 16 == 0,
                   "comet_attention_fwd: tensors must be 16-byte aligned");

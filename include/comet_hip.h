@@ -146,6 +146,11 @@ typedef struct comet_attn_args {
   void* o; int64_t so_b, so_h, so_l;
   float* lse;         /* contiguous [batch, heads, lq] */
   float scale;
+  /* optional inner batch (0 / 1 = none): batch index b addresses (b / batch_inner) * s*_b +
+   * (b % batch_inner) * s*_i -- attention over the tracks of a [B, N, T, C] tensor for every
+   * (b, t) (EfficientUpdateFormer space blocks, blocks.py:322-340) without permuting it */
+  int64_t batch_inner;
+  int64_t sq_i, sk_i, sv_i, so_i;
 } comet_attn_args;
 
 int comet_attention_fwd(const comet_attn_args* args, void* stream);

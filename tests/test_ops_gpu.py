@@ -484,3 +484,19 @@ def test_gemm_256_tile_transposed_and_split(la, lb, mnk):
     ops.gemm_raw(Ad, Bd, C, m=M, n=N, k=K, layout_a=la, lda=(K if la == 0 else M), layout_b=lb,
                  ldb=(K if lb == 0 else N), ldc=N)
     _close(C, ref, 1e-3, 1e-3 * math.sqrt(K), f"256 la={la} lb={lb} {mnk}")
+
+
+@pytest.mark.parametrize("D", [32, 48, 64])
+def test_attention_inner_batch_4d(D):
+    """[B, L, T, H*D] views: attention over L for every (b, t) (space blocks without permute)."""
+    ops = _ops()
+    B, L, T, H = 2, 70, 5, 3
+    C = H * D
+    x = _rand(B, L, T, 3 * C, seed=110).to(torch.bfloat16)
+    q, k, v = x[..., :C], x[..., C:2 * C], x[..., 2 * C:]
+    ref = torch.empty(B, L, T, C, dtype=torch.float64)
+    for t in range(T):
+        ref[:, :, t], _ = _attn_ref(q[:, :, t], k[:, :, t], v[:, :, t], H, D ** -0.5)
+    xd = x.to(DEV)
+    out = ops.attention(xd[..., :C], xd[..., C:2 * C], xd[..., 2 * C:], H)
+    _close(out, ref, 2e-2, 2e-2, f"inner-batch attention D={D}")
