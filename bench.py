@@ -98,6 +98,23 @@ def cpu_baseline(T, S_img, N):
                       f"oracle/comet_oracle.py, {dt:.1f} s, host '{cpu}'"}
 
 
+def pmc_traffic(instance, config):
+    """HBM bytes per launch of `instance` from the newest committed PMC summary
+    (profiles/r*_pmc.json, tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE per dispatch, from
+    separate rocprofv3 --pmc passes of this bench at the same config), else (None, None)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        try:
+            with open(path) as f:
+                j = json.load(f)
+        except (OSError, ValueError):
+            continue
+        r = j.get("instances", {}).get(instance, {})
+        if j.get("config") == config and "hbm_bytes_per_dispatch" in r:
+            return int(r["hbm_bytes_per_dispatch"]), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -157,24 +174,38 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    prof = PROF.summary()
+    prof_i = PROF.summary(instances=True)
+    prof = {}
+    for k, v in prof_i.items():
+        d = prof.setdefault(k.split("|", 1)[0], {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+        for f in d:
+            d[f] += v[f]
     if rank == 0:
         seqs = B * world * args.steps
         value = seqs / elapsed
-        # dominant kernel = largest total device time among profiled entry points
-        dom_name = max(prof, key=lambda k: prof[k]["ms"]) if prof else None
+        # dominant kernel = the kernel instance (one template instantiation, as rocprof names it)
+        # with the largest total device time; its launches are bracketed by HIP events on the
+        # launching stream (comet_amd/profiler.py)
+        dom_name = max(prof_i, key=lambda k: prof_i[k]["ms"]) if prof_i else None
         roof = None
         if dom_name:
-            d = prof[dom_name]
+            d = prof_i[dom_name]
             avg_ms = d["ms"] / d["launches"]
             ach = (d["flops"] / d["launches"]) / (avg_ms * 1e-3) / 1e12
+            traffic, tsrc = pmc_traffic(dom_name, {"batch": B, "frames": T, "image": args.image, "tracks": args.tracks})
             roof = {"bound": "mfma", "kernel": dom_name, "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                    "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE*2 + WRITE_SIZE)", "traffic_source": tsrc,
+                    "algorithmic_flop_per_launch": d["flops"] / d["launches"],
+                    "algorithmic_bytes_per_launch": d["bytes"] / d["launches"],
                     "launches_per_step": d["launches"] / args.steps, "avg_launch_ms": round(avg_ms, 4),
                     "share_of_step": round(d["ms"] / (elapsed * 1e3), 3)}
-        kernels = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] / args.steps,
-                       "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["ms"] > 0 else None}
-                   for k, v in prof.items()}
+        def table(p):
+            return {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] / args.steps,
+                        "tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2) if v["ms"] > 0 else None}
+                    for k, v in sorted(p.items(), key=lambda kv: -kv[1]["ms"])}
+        kernels = table(prof)
+        instances = table(prof_i)
         out = {
             "metric": "sequences/sec (BxT frames) COMET fwd+bwd, T=16 512^2",
             "value": round(value, 4), "unit": "sequences/s", "n_gpus": world, "steps": args.steps,
@@ -183,7 +214,7 @@ def main():
             "config": {"workload": "train_e2epose2.py fwd+bwd (BASELINE configs[2]): COMET tracker+DINOv2+head, loss, backward, "
                                    "grad all-reduce, clip 1.0, AdamW", "global_batch": B * world, "seq_len": T,
                        "image": args.image, "tracks": args.tracks, "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "final_loss": float(loss.item()) if loss is not None else None,
+            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "kernel_instances": instances, "final_loss": float(loss.item()) if loss is not None else None,
             "algorithmic_tflop_per_seq": 7.4773,
             "model_tflops": round(7.4773 * value, 2),
         }

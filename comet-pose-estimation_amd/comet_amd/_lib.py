@@ -83,6 +83,7 @@ SIGNATURES = {
     "comet_last_error": (ctypes.c_char_p, []),
     "comet_gemm": (_INT, [ctypes.POINTER(GemmArgs), c_vp]),
     "comet_gemm_workspace": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64)]),
+    "comet_gemm_plan": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_int32)]),
     "comet_conv2d_nhwc": (_INT, [ctypes.POINTER(ConvArgs), c_vp]),
     "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
                                    c_i64, _F, _INT, c_vp]),

@@ -86,7 +86,7 @@ def gemm_raw(a, b, c, *, m, n, k, layout_a, lda, layout_b, ldb, ldc, batch=(1, 1
     g.split_k = split_k
     lib = L.load()
     ws_bytes = ctypes.c_int64(0)
-    L.check(lib.comet_gemm_workspace(ctypes.byref(g), ctypes.byref(ws_bytes)), "comet_gemm_workspace")
+    L.check(lib.comet_gemm_plan(ctypes.byref(g), ctypes.byref(ws_bytes), _PLAN), "comet_gemm_plan")
     ws = None
     if ws_bytes.value > 0:  # split-K partials (torch caching allocator: no device sync)
         ws = torch.empty((ws_bytes.value + 3) // 4, device=c.device, dtype=torch.float32)
@@ -94,12 +94,30 @@ def gemm_raw(a, b, c, *, m, n, k, layout_a, lda, layout_b, ldb, ldc, batch=(1, 1
     e0 = PROF.start()
     L.check(lib.comet_gemm(ctypes.byref(g), stream()), "comet_gemm")
     if e0 is not None:
-        name = "comet_gemm"
+        name = "comet_gemm|" + _plan_name(layout_a, layout_b, cdt, c.dtype, ws_bytes.value > 0)
         if PROF.detail:
             name = (f"gemm L{layout_a}{layout_b} {a.dtype}->{c.dtype} M{m} N{n} K{k} b{batch[0]}x{batch[1]}"
                     f" act{act}{' bias' if bias is not None else ''}{' res' if resid is not None else ''}")
-        PROF.stop(e0, name, 2.0 * m * n * k * batch[0] * batch[1])
+        nb = batch[0] * batch[1]
+        io = (a.element_size() * m * k + b.element_size() * k * n +
+              c.element_size() * m * n * (1 + (resid is not None) + (aux is not None)))
+        PROF.stop(e0, name, 2.0 * m * n * k * nb, float(io * nb))
     return c
+
+
+_PLAN = (ctypes.c_int32 * 3)()
+
+
+def _plan_name(la, lb, cdt, odt, split):
+    """Kernel instance of the last comet_gemm_plan (matches the rocprof kernel names:
+    big::gemm_big_kernel<TC, BN, LA, LB, SPLIT>, bf::gemm_bf16_kernel<...>, gemm_skinny_kernel)."""
+    kind, bn = _PLAN[0], _PLAN[1]
+    out = "split" if split else ("bf16" if odt == torch.bfloat16 else "f32")
+    if kind == 0:
+        return f"skinny.{out}"
+    if kind == 1:
+        return f"big{bn}.L{la}{lb}.{out}"
+    return f"tile128.L{la}{lb}.{'bf16' if cdt == torch.bfloat16 else 'f32'}.{out}"
 
 
 def _cvt_ok(t, ld, st, contig):
@@ -253,7 +271,9 @@ def attention(q, k, v, heads, scale=None, out=None, lse=False):
     e0 = PROF.start()
     L.check(L.load().comet_attention_fwd(ctypes.byref(a), stream()), "attention")
     if e0 is not None:
-        name = f"attn fwd B{B} T{T} H{heads} Lq{Lq} Lk{Lk} D{D}" if PROF.detail else "comet_attention_fwd"
+        short = q.dtype == torch.bfloat16 and Lq <= 16 and Lk <= 16
+        name = (f"attn fwd B{B} T{T} H{heads} Lq{Lq} Lk{Lk} D{D}" if PROF.detail else
+                f"comet_attention_fwd|{'small' if short else 'tile'}.{'bf16' if q.dtype == torch.bfloat16 else 'f32'}.D{D}")
         PROF.stop(e0, name, 4.0 * B * T * heads * Lq * Lk * D)
     return (out, lse_t) if lse else out
 
@@ -281,7 +301,7 @@ def attention_bwd(q, k, v, o, lse, do, heads, scale, dq, dk, dv):
     e0 = PROF.start()
     L.check(L.load().comet_attention_bwd(ctypes.byref(a), stream()), "attention_bwd")
     if e0 is not None:
-        name = f"attn bwd B{B} H{heads} Lq{Lq} Lk{Lk} D{D}" if PROF.detail else "comet_attention_bwd"
+        name = f"attn bwd B{B} H{heads} Lq{Lq} Lk{Lk} D{D}" if PROF.detail else f"comet_attention_bwd|D{D}"
         PROF.stop(e0, name, 10.0 * B * heads * Lq * Lk * D)
 
 

@@ -38,10 +38,14 @@ class _Prof:
             self._pool += [a, b]
         self.records = []
 
-    def summary(self):
+    def summary(self, instances=False):
+        """{entry point: {launches, ms, flops, bytes}}; with instances=True keyed by the kernel
+        instance a call landed on ("comet_gemm|big256.L00.bf16") instead of the entry point."""
         torch.cuda.synchronize()
         out = {}
         for name, a, b, fl, nb in self.records:
+            if not instances:
+                name = name.split("|", 1)[0]
             d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
             d["launches"] += 1
             d["ms"] += a.elapsed_time(b)

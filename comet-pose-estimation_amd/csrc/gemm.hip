@@ -1400,6 +1400,19 @@ extern "C" int comet_gemm_workspace(const comet_gemm_args* args, int64_t* bytes)
   return COMET_OK;
 }
 
+extern "C" int comet_gemm_plan(const comet_gemm_args* args, int64_t* bytes, int32_t* plan) {
+  using namespace comet;
+  const int rc = validate(args);
+  if (rc != COMET_OK) return rc;
+  COMET_CHECK_ARG(bytes != nullptr && plan != nullptr, "comet_gemm_plan: null output");
+  const Plan p = make_plan(*args);
+  *bytes = plan_workspace(*args, p);
+  plan[0] = p.kind;
+  plan[1] = p.bn;
+  plan[2] = p.splits;
+  return COMET_OK;
+}
+
 extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   using namespace comet;
   const int rc = validate(args);

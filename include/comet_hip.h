@@ -84,6 +84,10 @@ typedef struct comet_gemm_args {
 int comet_gemm(const comet_gemm_args* args, void* stream);
 /* Workspace bytes comet_gemm needs for these arguments (0 when it will not split K). */
 int comet_gemm_workspace(const comet_gemm_args* args, int64_t* bytes);
+/* Same, plus the kernel plan comet_gemm will launch: plan[0] = 0 skinny (N <= 64),
+ * 1 256-row tile, 2 128 x 128 tile; plan[1] = the 256-row tile's BN; plan[2] = K splits.
+ * Lets a profiler name the kernel instance a call lands on (bench.py roofline). */
+int comet_gemm_plan(const comet_gemm_args* args, int64_t* bytes, int32_t* plan);
 
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM convolution on channels-last activations (nn.Conv2d of BasicEncoder /
