@@ -242,6 +242,189 @@ attn_fwd_kernel(const T* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_
   if (LSE && hg == 0) LSE[bh * lq + q] = (m_run + log2f(l_tot)) * LN2;
 }
 
+// bf16 forward, QG query groups of 16 per wave (one workgroup = 4 waves = 64*QG queries).
+// Same Sᵀ = K·Qᵀ / Oᵀ = Vᵀ·Pᵀ formulation as attn_fwd_kernel, trimmed for the VALU budget that
+// bounds attention at these head dims (a 16x16x32 MFMA leaves 8 issue cycles for the vector
+// unit; the softmax costs ~20 cycles of VALU per score-per-lane):
+//  * every K / Vᵀ fragment read from LDS feeds QG MFMAs (one per query group);
+//  * the softmax scale is folded into one FMA per score, exp2 is the bare v_exp_f32;
+//  * the key mask runs only on the last tile;
+//  * O is rescaled only when some lane's running max moved (exact: alpha == 1 otherwise).
+template <int D, int QG, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_l,
+                     const __bf16* __restrict__ K, int64_t sk_b, int64_t sk_h, int64_t sk_l,
+                     const __bf16* __restrict__ V, int64_t sv_b, int64_t sv_h, int64_t sv_l,
+                     __bf16* __restrict__ O, int64_t so_b, int64_t so_h, int64_t so_l,
+                     float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2, Inner in) {
+  constexpr int DA = ((D + 31) / 32) * 32, KP = DA + 8;
+  constexpr int DT = (D + 15) / 16, NQC = DA / 32;
+  constexpr int NVROW = D / 8, NVT = (64 * NVROW + 255) / 256;
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[64 * KP];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[64 * KP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 15, hg = lane >> 4;
+  const int64_t bh = blockIdx.y;
+  const int64_t b = bh / heads, h = bh % heads;
+  const int64_t bo = b / in.n, bi = b % in.n;
+  Q += bo * sq_b + bi * in.sq + h * sq_h;
+  K += bo * sk_b + bi * in.sk + h * sk_h;
+  V += bo * sv_b + bi * in.sv + h * sv_h;
+  O += bo * so_b + bi * in.so + h * so_h;
+
+  if constexpr (DA != D) {  // pad columns [D, DA) of K stay zero for the whole kernel
+    for (int i = tid; i < 64 * KP; i += 256) Ks[i] = __bf16(0.f);
+  }
+
+  bf16x8 qf[QG][NQC];
+  int qrow[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    qrow[g] = blockIdx.x * (64 * QG) + (wid * QG + g) * 16 + li;
+#pragma unroll
+    for (int c = 0; c < NQC; ++c) {
+      const int d0 = 32 * c + 8 * hg;
+      qf[g][c] = (qrow[g] < lq && d0 < D) ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow[g] * sq_l + d0) : bf16x8{};
+    }
+  }
+  f32x4 o[QG][DT];
+  float m_run[QG], l_run[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    m_run[g] = -INFINITY;
+    l_run[g] = 0.f;
+#pragma unroll
+    for (int i = 0; i < DT; ++i) o[g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const int ntiles = (lk + 63) / 64;
+  uint4 kreg[NVT], vreg[NVT];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NVT; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / NVROW, cv = (idx % NVROW) * 8;
+      const int key = t * 64 + row;
+      const bool ok = idx < 64 * NVROW && key < lk;
+      kreg[i] = ok ? *reinterpret_cast<const uint4*>(K + (int64_t)key * sk_l + cv) : uint4{0, 0, 0, 0};
+      vreg[i] = ok ? *reinterpret_cast<const uint4*>(V + (int64_t)key * sv_l + cv) : uint4{0, 0, 0, 0};
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < NVT; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < 64 * NVROW) {
+        const int row = idx / NVROW, cv = (idx % NVROW) * 8;
+        *reinterpret_cast<uint4*>(Ks + row * KP + cv) = kreg[i];
+        *reinterpret_cast<uint4*>(Vs + row * KP + cv) = vreg[i];
+      }
+    }
+  };
+
+  // one 64-key tile; MASK only for a ragged last tile
+  auto tile = [&](int t, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
+    f32x4 s[QG][4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+#pragma unroll
+      for (int g = 0; g < QG; ++g) s[g][st] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const __bf16* krow = Ks + (st * 16 + li) * KP + 8 * hg;
+#pragma unroll
+      for (int c = 0; c < NQC; ++c) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(krow + 32 * c);
+#pragma unroll
+        for (int g = 0; g < QG; ++g) s[g][st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[g][c], s[g][st], 0, 0, 0);
+      }
+    }
+    bf16x8 pf[QG][2];
+#pragma unroll
+    for (int g = 0; g < QG; ++g) {
+      if constexpr (MASK) {
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (t * 64 + st * 16 + 4 * hg + r >= lk) s[g][st][r] = -INFINITY;
+      }
+      float mt = fmaxf(fmaxf(s[g][0][0], s[g][0][1]), fmaxf(s[g][0][2], s[g][0][3]));
+#pragma unroll
+      for (int st = 1; st < 4; ++st)
+        mt = fmaxf(fmaxf(mt, fmaxf(s[g][st][0], s[g][st][1])), fmaxf(s[g][st][2], s[g][st][3]));
+      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float m_new = fmaxf(m_run[g], mt * scale_log2);
+      if (__ballot(m_new > m_run[g]) != 0) {
+        const float alpha = __builtin_amdgcn_exp2f(m_run[g] - m_new);
+        l_run[g] *= alpha;
+#pragma unroll
+        for (int i = 0; i < DT; ++i) o[g][i] *= alpha;
+        m_run[g] = m_new;
+      }
+      float ls = 0.f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[g][st][r], scale_log2, -m_new));
+          s[g][st][r] = p;
+          ls += p;
+        }
+      l_run[g] += ls;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        pf[g][u] = __builtin_shufflevector(__builtin_convertvector(s[g][2 * u], bf16x4),
+                                           __builtin_convertvector(s[g][2 * u + 1], bf16x4), 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+    const int qq = li >> 2, pp = li & 3;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const __bf16* a0 = Vs + (16 * (2 * u) + 4 * hg + qq) * KP + 16 * dt + 4 * pp;
+        const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 16 * KP));
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int g = 0; g < QG; ++g) o[g][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[g][u], o[g][dt], 0, 0, 0);
+      }
+    }
+  };
+
+  // full tiles unmasked; the last tile (peeled: one masked instantiation outside the loop keeps
+  // the loop's register allocation that of the unmasked body) masks keys >= lk
+  gload(0);
+  for (int t = 0; t < ntiles - 1; ++t) {
+    __syncthreads();  // previous tile consumed (and LDS zeroing done)
+    lstore();
+    __syncthreads();
+    gload(t + 1);
+    tile(t, std::false_type{});
+  }
+  __syncthreads();
+  lstore();
+  __syncthreads();
+  tile(ntiles - 1, std::true_type{});
+
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    float l_tot = l_run[g];
+    l_tot += __shfl_xor(l_tot, 16, 64);
+    l_tot += __shfl_xor(l_tot, 32, 64);
+    if (qrow[g] >= lq) continue;
+    const float inv = 1.f / l_tot;
+    __bf16* orow = O + (int64_t)qrow[g] * so_l;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int d0 = 16 * dt + 4 * hg;
+      if (d0 < D) *reinterpret_cast<bf16x4*>(orow + d0) = __builtin_convertvector(o[g][dt] * inv, bf16x4);
+    }
+    if (LSE && hg == 0) LSE[bh * lq + qrow[g]] = (m_run[g] + log2f(l_tot)) * LN2;
+  }
+}
+
 // Short sequences (Lq, Lk <= 16: the tracker's per-track time attention over S = 16 frames,
 // blocks.py:312-321): one wave per (batch, head) instead of a 64 x 64 tile that would be 1/16
 // occupied. Sᵀ = K·Qᵀ in one 16x16 MFMA tile per 32 of d (K and Q fragments straight from
@@ -341,6 +524,22 @@ int launch_fwd(const comet_attn_args& a, hipStream_t s) {
   return COMET_OK;
 }
 
+template <int D>
+int launch_fwd_bf16(const comet_attn_args& a, hipStream_t s) {
+  // two query groups per wave when both sequences span several tiles (measured on the COMET
+  // shapes, tools/attn_bench.py: DINO 581x581 D64 497 -> 317 us, head 577x577 D96 419 -> 273 us);
+  // with a single key tile the halved grid costs more than the K/V fragment reuse saves
+  const bool two = a.lq > 64 && a.lk > 64;
+  dim3 grid((unsigned)cdiv(a.lq, two ? 128 : 64), (unsigned)(a.batch * a.heads));
+  auto kern = two ? attn_fwd_bf16_kernel<D, 2, (D > 64 ? 3 : 2)> : attn_fwd_bf16_kernel<D, 1, 4>;
+  hipLaunchKernelGGL(kern, grid, dim3(256), 0, s,
+                     (const __bf16*)a.q, a.sq_b, a.sq_h, a.sq_l, (const __bf16*)a.k, a.sk_b, a.sk_h, a.sk_l,
+                     (const __bf16*)a.v, a.sv_b, a.sv_h, a.sv_l, (__bf16*)a.o, a.so_b, a.so_h, a.so_l,
+                     a.lse, (int)a.heads, (int)a.lq, (int)a.lk, a.scale * LOG2E, inner_of(a));
+  COMET_CHECK_LAUNCH("comet_attention_fwd");
+  return COMET_OK;
+}
+
 template <typename T>
 int dispatch_d(const comet_attn_args& a, hipStream_t s) {
   if (std::is_same<T, __bf16>::value && a.lq <= 16 && a.lk <= 16 && a.batch * a.heads < (1ll << 31) * 4) {
@@ -349,6 +548,15 @@ int dispatch_d(const comet_attn_args& a, hipStream_t s) {
       case 48: return launch_small<48>(a, s);
       case 64: return launch_small<64>(a, s);
       case 96: return launch_small<96>(a, s);
+      default: break;
+    }
+  }
+  if (std::is_same<T, __bf16>::value) {
+    switch (a.head_dim) {
+      case 32: return launch_fwd_bf16<32>(a, s);
+      case 48: return launch_fwd_bf16<48>(a, s);
+      case 64: return launch_fwd_bf16<64>(a, s);
+      case 96: return launch_fwd_bf16<96>(a, s);
       default: break;
     }
   }

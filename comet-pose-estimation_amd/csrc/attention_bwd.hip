@@ -80,15 +80,20 @@ __device__ __forceinline__ void load_frags(const __bf16* base, int64_t sl, int r
   }
 }
 
-// ---------------------------------------------------------------- dK, dV
-template <int D>
+// ---------------------------------------------------------------- dK, dV  /  dQ
+// G row groups per wave (every LDS fragment feeds G MFMAs; G = 1 is dispatched: at G = 2 the
+// D = 96 instances fall to 1-2 waves per SIMD), the 64-row tile processed in two 32-row halves
+// to bound the live S / dP registers, lse / Δ read as float4, and
+// P = exp2(fma(s, scale·log2e, -lse·log2e)) on the bare v_exp_f32.
+template <int D, int G>
 __global__ void __launch_bounds__(256)
-attn_bwd_dkdv_kernel(BwdPtrs p) {
+attn_bwd_dkdv2_kernel(BwdPtrs p) {
   typedef BCfg<D> C;
   constexpr int KP = C::KP, NQC = C::NQC, DT = C::DT, NVROW = C::NVROW, NVT = C::NVT;
   __shared__ __attribute__((aligned(16))) __bf16 Qs[64 * KP];
   __shared__ __attribute__((aligned(16))) __bf16 Gs[64 * KP];  // dO tile
-  __shared__ float lse_s[64], dl_s[64];
+  __shared__ __attribute__((aligned(16))) float lse_s[64];
+  __shared__ __attribute__((aligned(16))) float dl_s[64];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 15, g = lane >> 4, qq = li >> 2, pp = li & 3;
@@ -96,21 +101,26 @@ attn_bwd_dkdv_kernel(BwdPtrs p) {
   const __bf16* Q = p.q + b * p.sq_b + h * p.sq_h;
   const __bf16* K = p.k + b * p.sk_b + h * p.sk_h;
   const __bf16* V = p.v + b * p.sv_b + h * p.sv_h;
-  const __bf16* G = p.dout + b * p.sd_b + h * p.sd_h;
+  const __bf16* Gd = p.dout + b * p.sd_b + h * p.sd_h;
   const float* LSE = p.lse + bh * p.lq;
   const float* DL = p.delta + bh * p.lq;
   const float sl2 = p.scale * LOG2E_B;
 
-  for (int i = tid; i < 64 * KP; i += 256) { Qs[i] = __bf16(0.f); Gs[i] = __bf16(0.f); }
+  if constexpr (C::DA != D) {  // pad columns of the Q / dO tiles read by the S / dP MFMAs
+    for (int i = tid; i < 64 * KP; i += 256) { Qs[i] = __bf16(0.f); Gs[i] = __bf16(0.f); }
+  }
 
-  const int key = blockIdx.x * 64 + wid * 16 + li;
-  bf16x8 kf[NQC], vf[NQC];
-  load_frags<D>(K, p.sk_l, key, key < p.lk, g, kf);
-  load_frags<D>(V, p.sv_l, key, key < p.lk, g, vf);
-
-  f32x4 dv[DT], dk[DT];
+  int key0[G];
+  bf16x8 kf[G][NQC], vf[G][NQC];
+  f32x4 dv[G][DT], dk[G][DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) { dv[i] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  for (int k = 0; k < G; ++k) {
+    key0[k] = blockIdx.x * (64 * G) + (wid * G + k) * 16;
+    load_frags<D>(K, p.sk_l, key0[k] + li, key0[k] + li < p.lk, g, kf[k]);
+    load_frags<D>(V, p.sv_l, key0[k] + li, key0[k] + li < p.lk, g, vf[k]);
+#pragma unroll
+    for (int i = 0; i < DT; ++i) { dv[k][i] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[k][i] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  }
 
   uint4 qreg[NVT], greg[NVT];
   float lreg = 0.f, dreg = 0.f;
@@ -120,13 +130,9 @@ attn_bwd_dkdv_kernel(BwdPtrs p) {
       const int idx = tid + i * 256;
       const int row = idx / NVROW, cv = (idx % NVROW) * 8;
       const int q = t * 64 + row;
-      if (idx < 64 * NVROW && q < p.lq) {
-        qreg[i] = *reinterpret_cast<const uint4*>(Q + (int64_t)q * p.sq_l + cv);
-        greg[i] = *reinterpret_cast<const uint4*>(G + (int64_t)q * p.sd_l + cv);
-      } else {
-        qreg[i] = uint4{0, 0, 0, 0};
-        greg[i] = uint4{0, 0, 0, 0};
-      }
+      const bool ok = idx < 64 * NVROW && q < p.lq;
+      qreg[i] = ok ? *reinterpret_cast<const uint4*>(Q + (int64_t)q * p.sq_l + cv) : uint4{0, 0, 0, 0};
+      greg[i] = ok ? *reinterpret_cast<const uint4*>(Gd + (int64_t)q * p.sd_l + cv) : uint4{0, 0, 0, 0};
     }
     if (tid < 64) {
       const int q = t * 64 + tid;
@@ -154,62 +160,72 @@ attn_bwd_dkdv_kernel(BwdPtrs p) {
     lstore();
     __syncthreads();
     if (t + 1 < ntiles) gload(t + 1);
-
-    // S, dP with the query on the row: C[q = 16st + 4g + r][key = li]
-    f32x4 s[4], dp[4];
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      s[st] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[st] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < NQC; ++c) {
-        const bf16x8 qa = frag_rows(Qs, (st * 16 + li) * KP, 32 * c + 8 * g);
-        const bf16x8 ga = frag_rows(Gs, (st * 16 + li) * KP, 32 * c + 8 * g);
-        s[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[c], s[st], 0, 0, 0);
-        dp[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, vf[c], dp[st], 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ql = st * 16 + 4 * g + r;
-        const float pr = exp2f(s[st][r] * sl2 - lse_s[ql]);
-        s[st][r] = pr;                          // P
-        dp[st][r] = pr * (dp[st][r] - dl_s[ql]);  // dS (unscaled)
-      }
-    }
-    // dV += Pᵀ dO, dK += dSᵀ Q   (k = queries, permuted order)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const bf16x8 pa = pack_operand(s[2 * u], s[2 * u + 1]);
-      const bf16x8 da = pack_operand(dp[2 * u], dp[2 * u + 1]);
+      // S, dP of queries 32u + 16j + 4g + r (row) x the wave's keys (lane)
+      f32x4 s[G][2], dp[G][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int st = 2 * u + j;
+#pragma unroll
+        for (int k = 0; k < G; ++k) { s[k][j] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[k][j] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+        for (int c = 0; c < NQC; ++c) {
+          const bf16x8 qa = frag_rows(Qs, (st * 16 + li) * KP, 32 * c + 8 * g);
+          const bf16x8 ga = frag_rows(Gs, (st * 16 + li) * KP, 32 * c + 8 * g);
+#pragma unroll
+          for (int k = 0; k < G; ++k) {
+            s[k][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[k][c], s[k][j], 0, 0, 0);
+            dp[k][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, vf[k][c], dp[k][j], 0, 0, 0);
+          }
+        }
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(lse_s + st * 16 + 4 * g);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(dl_s + st * 16 + 4 * g);
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pr = __builtin_amdgcn_exp2f(__builtin_fmaf(s[k][j][r], sl2, -l4[r]));
+            s[k][j][r] = pr;                         // P
+            dp[k][j][r] = pr * (dp[k][j][r] - d4[r]);  // dS (unscaled)
+          }
+      }
+      bf16x8 pa[G], da[G];
+#pragma unroll
+      for (int k = 0; k < G; ++k) { pa[k] = pack_operand(s[k][0], s[k][1]); da[k] = pack_operand(dp[k][0], dp[k][1]); }
+      // dV += Pᵀ dO, dK += dSᵀ Q over these 32 queries (permuted k order)
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const bf16x8 gb = frag_tr<KP>(Gs, u, g, qq, pp, 16 * dt);
         const bf16x8 qb = frag_tr<KP>(Qs, u, g, qq, pp, 16 * dt);
-        dv[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, gb, dv[dt], 0, 0, 0);
-        dk[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da, qb, dk[dt], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+          dv[k][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[k], gb, dv[k][dt], 0, 0, 0);
+          dk[k][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(da[k], qb, dk[k][dt], 0, 0, 0);
+        }
       }
     }
   }
 
-  // C layout: row = key 4g + r of the wave's 16, col = d 16dt + li
   __bf16* dK = p.dk + b * p.sdk_b + h * p.sdk_h;
   __bf16* dV = p.dv + b * p.sdv_b + h * p.sdv_h;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int kr = blockIdx.x * 64 + wid * 16 + 4 * g + r;
-    if (kr >= p.lk) continue;
+  for (int k = 0; k < G; ++k)
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      dV[(int64_t)kr * p.sdv_l + 16 * dt + li] = static_cast<__bf16>(dv[dt][r]);
-      dK[(int64_t)kr * p.sdk_l + 16 * dt + li] = static_cast<__bf16>(dk[dt][r] * p.scale);
+    for (int r = 0; r < 4; ++r) {
+      const int kr = key0[k] + 4 * g + r;
+      if (kr >= p.lk) continue;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        dV[(int64_t)kr * p.sdv_l + 16 * dt + li] = static_cast<__bf16>(dv[k][dt][r]);
+        dK[(int64_t)kr * p.sdk_l + 16 * dt + li] = static_cast<__bf16>(dk[k][dt][r] * p.scale);
+      }
     }
-  }
 }
 
-// ---------------------------------------------------------------- dQ
-template <int D>
+template <int D, int G>
 __global__ void __launch_bounds__(256)
-attn_bwd_dq_kernel(BwdPtrs p) {
+attn_bwd_dq2_kernel(BwdPtrs p) {
   typedef BCfg<D> C;
   constexpr int KP = C::KP, NQC = C::NQC, DT = C::DT, NVROW = C::NVROW, NVT = C::NVT;
   __shared__ __attribute__((aligned(16))) __bf16 Ks[64 * KP];
@@ -221,22 +237,28 @@ attn_bwd_dq_kernel(BwdPtrs p) {
   const __bf16* Q = p.q + b * p.sq_b + h * p.sq_h;
   const __bf16* K = p.k + b * p.sk_b + h * p.sk_h;
   const __bf16* V = p.v + b * p.sv_b + h * p.sv_h;
-  const __bf16* G = p.dout + b * p.sd_b + h * p.sd_h;
+  const __bf16* Gd = p.dout + b * p.sd_b + h * p.sd_h;
   const float sl2 = p.scale * LOG2E_B;
 
-  for (int i = tid; i < 64 * KP; i += 256) { Ks[i] = __bf16(0.f); Vs[i] = __bf16(0.f); }
+  if constexpr (C::DA != D) {
+    for (int i = tid; i < 64 * KP; i += 256) { Ks[i] = __bf16(0.f); Vs[i] = __bf16(0.f); }
+  }
 
-  const int q = blockIdx.x * 64 + wid * 16 + li;
-  const bool qok = q < p.lq;
-  bf16x8 qf[NQC], gf[NQC];
-  load_frags<D>(Q, p.sq_l, q, qok, g, qf);
-  load_frags<D>(G, p.sd_l, q, qok, g, gf);
-  const float lse2 = qok ? p.lse[bh * p.lq + q] * LOG2E_B : INFINITY;
-  const float dl = qok ? p.delta[bh * p.lq + q] : 0.f;
-
-  f32x4 acc[DT];
+  int qrow[G];
+  bf16x8 qf[G][NQC], gf[G][NQC];
+  float lse2[G], dl[G];
+  f32x4 acc[G][DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < G; ++k) {
+    qrow[k] = blockIdx.x * (64 * G) + (wid * G + k) * 16 + li;
+    const bool ok = qrow[k] < p.lq;
+    load_frags<D>(Q, p.sq_l, qrow[k], ok, g, qf[k]);
+    load_frags<D>(Gd, p.sd_l, qrow[k], ok, g, gf[k]);
+    lse2[k] = ok ? p.lse[bh * p.lq + qrow[k]] * LOG2E_B : INFINITY;
+    dl[k] = ok ? p.delta[bh * p.lq + qrow[k]] : 0.f;
+#pragma unroll
+    for (int i = 0; i < DT; ++i) acc[k][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   uint4 kreg[NVT], vreg[NVT];
   auto gload = [&](int t) {
@@ -245,13 +267,9 @@ attn_bwd_dq_kernel(BwdPtrs p) {
       const int idx = tid + i * 256;
       const int row = idx / NVROW, cv = (idx % NVROW) * 8;
       const int kk = t * 64 + row;
-      if (idx < 64 * NVROW && kk < p.lk) {
-        kreg[i] = *reinterpret_cast<const uint4*>(K + (int64_t)kk * p.sk_l + cv);
-        vreg[i] = *reinterpret_cast<const uint4*>(V + (int64_t)kk * p.sv_l + cv);
-      } else {
-        kreg[i] = uint4{0, 0, 0, 0};
-        vreg[i] = uint4{0, 0, 0, 0};
-      }
+      const bool ok = idx < 64 * NVROW && kk < p.lk;
+      kreg[i] = ok ? *reinterpret_cast<const uint4*>(K + (int64_t)kk * p.sk_l + cv) : uint4{0, 0, 0, 0};
+      vreg[i] = ok ? *reinterpret_cast<const uint4*>(V + (int64_t)kk * p.sv_l + cv) : uint4{0, 0, 0, 0};
     }
   };
   auto lstore = [&]() {
@@ -273,46 +291,55 @@ attn_bwd_dq_kernel(BwdPtrs p) {
     lstore();
     __syncthreads();
     if (t + 1 < ntiles) gload(t + 1);
-
-    // Sᵀ, dPᵀ with the query on the lane: C[key = 16st + 4g + r][q = li]
-    f32x4 s[4], dp[4];
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      s[st] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[st] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < NQC; ++c) {
-        const bf16x8 ka = frag_rows(Ks, (st * 16 + li) * KP, 32 * c + 8 * g);
-        const bf16x8 va = frag_rows(Vs, (st * 16 + li) * KP, 32 * c + 8 * g);
-        s[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[c], s[st], 0, 0, 0);
-        dp[st] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, gf[c], dp[st], 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int kk = t * 64 + st * 16 + 4 * g + r;
-        const float pr = kk < p.lk ? exp2f(s[st][r] * sl2 - lse2) : 0.f;
-        dp[st][r] = pr * (dp[st][r] - dl);  // dS (unscaled)
-      }
-    }
-    // dQᵀ += Kᵀ dSᵀ  (k = keys, permuted order)
+    const bool ragged = t * 64 + 64 > p.lk;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const bf16x8 db = pack_operand(dp[2 * u], dp[2 * u + 1]);
+      f32x4 dp[G][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int st = 2 * u + j;
+        f32x4 s[G];
+#pragma unroll
+        for (int k = 0; k < G; ++k) { s[k] = f32x4{0.f, 0.f, 0.f, 0.f}; dp[k][j] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+#pragma unroll
+        for (int c = 0; c < NQC; ++c) {
+          const bf16x8 ka = frag_rows(Ks, (st * 16 + li) * KP, 32 * c + 8 * g);
+          const bf16x8 va = frag_rows(Vs, (st * 16 + li) * KP, 32 * c + 8 * g);
+#pragma unroll
+          for (int k = 0; k < G; ++k) {
+            s[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, qf[k][c], s[k], 0, 0, 0);
+            dp[k][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, gf[k][c], dp[k][j], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float pr = __builtin_amdgcn_exp2f(__builtin_fmaf(s[k][r], sl2, -lse2[k]));
+            if (ragged && t * 64 + st * 16 + 4 * g + r >= p.lk) pr = 0.f;
+            dp[k][j][r] = pr * (dp[k][j][r] - dl[k]);  // dS (unscaled)
+          }
+      }
+      // dQᵀ += Kᵀ dSᵀ over these 32 keys (permuted k order)
+      bf16x8 db[G];
+#pragma unroll
+      for (int k = 0; k < G; ++k) db[k] = pack_operand(dp[k][0], dp[k][1]);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const bf16x8 ka = frag_tr<KP>(Ks, u, g, qq, pp, 16 * dt);
-        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, db, acc[dt], 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < G; ++k) acc[k][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ka, db[k], acc[k][dt], 0, 0, 0);
       }
     }
   }
 
-  if (!qok) return;
-  // C layout: row = d 16dt + 4g + r, col = query li
-  __bf16* dQ = p.dq + b * p.sdq_b + h * p.sdq_h + (int64_t)q * p.sdq_l;
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    const bf16x4 w = __builtin_convertvector(acc[dt] * p.scale, bf16x4);
-    *reinterpret_cast<bf16x4*>(dQ + 16 * dt + 4 * g) = w;
+  for (int k = 0; k < G; ++k) {
+    if (qrow[k] >= p.lq) continue;
+    __bf16* dQ = p.dq + b * p.sdq_b + h * p.sdq_h + (int64_t)qrow[k] * p.sdq_l;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+      *reinterpret_cast<bf16x4*>(dQ + 16 * dt + 4 * g) = __builtin_convertvector(acc[k][dt] * p.scale, bf16x4);
   }
 }
 
@@ -344,9 +371,11 @@ attn_delta_bf16_kernel(const __bf16* __restrict__ dO, const __bf16* __restrict__
 
 template <int D>
 int launch_bwd(const BwdPtrs& p, int64_t bh, hipStream_t s) {
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D>), dim3((unsigned)cdiv(p.lk, 64), (unsigned)bh), dim3(256), 0, s, p);
+  // one row group per wave: at G = 2 the D = 96 kernels drop to 1-2 waves per SIMD and lose
+  // more than the halved LDS traffic gains (tools/attn_bench.py)
+  hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<D, 1>), dim3((unsigned)cdiv(p.lk, 64), (unsigned)bh), dim3(256), 0, s, p);
   COMET_CHECK_LAUNCH("comet_attention_bwd (dk, dv)");
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D>), dim3((unsigned)cdiv(p.lq, 64), (unsigned)bh), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((attn_bwd_dq2_kernel<D, 1>), dim3((unsigned)cdiv(p.lq, 64), (unsigned)bh), dim3(256), 0, s, p);
   COMET_CHECK_LAUNCH("comet_attention_bwd (dq)");
   return COMET_OK;
 }

@@ -85,9 +85,11 @@ def instance(name):
             return "comet_conv2d_nhwc|skinny"
         if base == "attn_fwd_kernel":
             return f"comet_attention_fwd|tile.{a[0]}.D{a[1]}"
+        if base == "attn_fwd_bf16_kernel":
+            return f"comet_attention_fwd|tile.bf16.D{a[0]}"
         if base == "attn_small_kernel":
             return f"comet_attention_fwd|small.bf16.D{a[0]}"
-        if base in ("attn_bwd_dkdv_kernel", "attn_bwd_dq_kernel", "attn_delta_bf16_kernel"):
+        if base in ("attn_bwd_dkdv2_kernel", "attn_bwd_dq2_kernel", "attn_delta_bf16_kernel"):
             return f"comet_attention_bwd|{base}"
     except IndexError:
         return None
