@@ -117,6 +117,8 @@ def _plan_name(la, lb, cdt, odt, split):
         return f"skinny.{out}"
     if kind == 1:
         return f"big{bn}.L{la}{lb}.{out}"
+    if kind == 3:
+        return f"pp256.L{la}{lb}.{out}"
     return f"tile128.L{la}{lb}.{'bf16' if cdt == torch.bfloat16 else 'f32'}.{out}"
 
 

@@ -944,6 +944,341 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
 }
 }  // namespace big
 
+// ============================== persistent 256 x 256 kernel ======================================
+// The forward Linear shapes (k-contiguous bf16 A and B, K % 64 == 0). What the 256-row kernel above
+// loses per tile (measured on M 74368, N 3072, K 768: MFMA busy 28 % of the SIMD cycles) is the
+// lock-step [barrier -> glds burst + ds_read burst -> wait -> MFMA] body of its waves, the
+// park-in-LDS epilogue and the tile prologue's load latency. Here:
+//  * each 32-deep k-step of a wave is one MFMA stream with the next k-step's fragment reads (and,
+//    in the second k-step, this wave's LDS-DMA pieces of k-tile q+2) issued one by one between the
+//    MFMAs (sched_group_barrier), fragments double-buffered in registers;
+//  * one barrier per 64-deep k-tile, between its two k-steps: it retires every wave's reads of
+//    buffer q&1 (which the second k-step then refills with k-tile q+2) and every wave's LDS-DMA of
+//    k-tile q+1 (whose first-k-step fragments the second k-step reads);
+//  * persistent: one workgroup per CU walks its tiles (XCD-banded order) and the k-tile stream runs
+//    on across tile boundaries, so the next tile's first two k-tiles load during this epilogue;
+//  * Cᵀ = W·Xᵀ per MFMA (operands swapped): a lane holds 4 consecutive output columns of one row
+//    and the epilogue stores straight from the accumulators (no LDS park).
+// NW = 8: 2 x 4 waves of 128 x 64 (two waves per SIMD); NW = 4: 2 x 2 waves of 128 x 128.
+namespace w4 {
+constexpr int BM = 256, BK = 64;
+constexpr int WGM = 8;  // logical tiles run down groups of WGM tile rows, column by column
+
+// logical tile -> (tile row, tile column): an XCD's 32 consecutive tiles form an 8 x 4 patch
+// (A blocks shared by 4 workgroups, B blocks by 8) instead of a 32-wide strip of one tile row
+__device__ __forceinline__ void tile_rc(int L, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int gsz = WGM * tiles_n, grp = L / gsz, rem = L - grp * gsz;
+  const int rows = min(WGM, tiles_m - grp * WGM);
+  tm = grp * WGM + rem % rows;
+  tn = rem / rows;
+}
+constexpr int ASTAGE = BM * BK;  // bf16 elements of one operand image (32 KiB)
+constexpr int BUF = 2 * ASTAGE;  // A + B images of one k-tile (64 KiB)
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int SG_MFMA = 0x008, SG_DSR = 0x100, SG_VMR = 0x020;
+
+template <typename TC, int ACT, bool HASR, int NW>
+__global__ void __launch_bounds__(NW * 64, 1)
+gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
+               TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, int ntiles,
+               Epi epi) {
+  constexpr int WN = NW / 2;        // wave grid 2 x WN
+  constexpr int WCOLS = BM / WN;    // wave tile columns (64 or 128)
+  constexpr int NI = WCOLS / 16;    // column fragments per wave (4 or 8)
+  constexpr int PPW = 32 / NW;      // LDS-DMA pieces per operand per wave and k-tile (4 or 8)
+  constexpr int NMF = 8 * NI;       // MFMAs per k-step (32 or 64)
+  constexpr int NRD = 8 + NI;       // fragment reads per k-step (12 or 16)
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid / WN, wc = wid % WN;
+  const int li = lane & 15, g = lane >> 4;
+  const int nk = (int)(K / BK);
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int tiles_m = ntiles / tiles_n;
+  const bool single = ntiles <= G;
+  const int off = single ? xcd_remap(bid, G) : (bid & 7) * (G >> 3) + (bid >> 3);
+  const int my_tiles = single ? 1 : (off < ntiles ? (ntiles - off + G - 1) / G : 0);
+  const int T = my_tiles * nk;
+  if (T == 0) return;
+
+  // ---- load stream: a wave issues LDS-DMA pieces wid*PPW + p of each operand image (8 rows x 64 k
+  // = 1 KiB each; 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)); source rows clamped (tails
+  // re-read the last row, never stored)
+  const int prow = wid * PPW * 8 + (lane >> 3);                 // + p * 8
+  const int lch0 = ((lane & 7) ^ ((lane >> 4) & 3)) * 8;        // chunk column, even p
+  const int lch1 = ((lane & 7) ^ (4 | ((lane >> 4) & 3))) * 8;  // odd p
+  // load-stream state: the k-tile the next issue_cur() loads (tile ld_it of this workgroup, k-tile
+  // ld_kt of it); per tile, uniform row-block bases and per-lane 32-bit element offsets
+  int ld_it = 0, ld_kt = 0;
+  const __bf16* ldA = A;
+  const __bf16* ldB = B;
+  int offA[PPW], offB[PPW];
+  auto set_load_tile = [&](int it) {
+    int tm, tn;
+    tile_rc(off + it * G, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * BM, n0 = tn * BM;
+    ldA = A + (int64_t)m0 * lda;
+    ldB = B + (int64_t)n0 * ldb;
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) {
+      const int r = prow + p * 8, lch = (p & 1) ? lch1 : lch0;
+      offA[p] = (min(m0 + r, (int)M - 1) - m0) * (int)lda + lch;
+      offB[p] = (min(n0 + r, (int)N - 1) - n0) * (int)ldb + lch;
+    }
+  };
+  auto issue_cur = [&](int buf) {
+    const __bf16* pa = ldA + ld_kt * BK;
+    const __bf16* pb = ldB + ld_kt * BK;
+#pragma unroll
+    for (int p = 0; p < PPW; ++p) {
+      __bf16* img = smem + buf * BUF + (wid * PPW + p) * 512;
+      __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)img, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]), (lds_void*)(img + ASTAGE), 16, 0, 0);
+    }
+  };
+  // past the last k-tile the stream keeps re-loading it (into a buffer nothing reads again)
+  auto advance = [&]() {
+    if (++ld_kt == nk) {
+      if (ld_it + 1 < my_tiles) { ld_kt = 0; set_load_tile(++ld_it); }
+      else ld_kt = nk - 1;
+    }
+  };
+
+  bf16x8 a0[8], b0[NI], a1[8], b1[NI];
+  auto read_frags = [&](int buf, int s, bf16x8 (&af)[8], bf16x8 (&bf)[NI]) {
+    const __bf16* img = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = big::frag(img, wr * 128 + i * 16 + li, 4 * s + g);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) bf[j] = big::frag(img + ASTAGE, wc * WCOLS + j * 16 + li, 4 * s + g);
+  };
+
+  f32x4 acc[8][NI];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mfmas = [&](const bf16x8 (&af)[8], const bf16x8 (&bf)[NI]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+  };
+
+  int pend = 0;  // 1: the last epilogue's stores are the newest VMEM ops (count known)
+  // ---- prologue: k-tiles 0 and 1 in flight, k-tile 0 landed, its first-k-step fragments read
+  set_load_tile(0);
+  issue_cur(0);
+  advance();
+  if (T > 1) {
+    issue_cur(1);
+    advance();
+    if constexpr (PPW == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_barrier" ::: "memory");
+  read_frags(0, 0, a0, b0);
+
+  for (int q = 0; q < T; ++q) {
+    // ---- k-step 0 of k-tile q: MFMAs on (a0, b0), reads of the k-step-1 fragments (a1, b1)
+    read_frags(q & 1, 1, a1, b1);
+    mfmas(a0, b0);
+#pragma unroll
+    for (int t = 0; t < NRD; ++t) {
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, NMF / NRD - 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(SG_MFMA, NMF % NRD, 0);
+    // every wave's reads of buffer q&1 and LDS-DMA of k-tile q+1 are done past this barrier; after
+    // an interior tile's epilogue its stores (all issued after that LDS-DMA) stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (pend) {
+      constexpr int E = 8 * NI * (1 + (HASR ? 1 : 0)) + 8 * NI;  // C stores (+ resid loads) (+ aux stores)
+      if (epi.aux) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E > 63 ? 63 : E) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E - 8 * NI > 63 ? 63 : E - 8 * NI) : "memory");
+      pend = 0;
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- k-step 1: MFMAs on (a1, b1); LDS-DMA of k-tile q+2 into buffer q&1 (past the end of the
+    // stream: a re-load of the last k-tile that nothing reads); reads of k-tile q+1's k-step-0
+    // fragments (a0, b0) from buffer (q+1)&1 (garbage past the end, never used). Branch-free.
+    {
+      issue_cur(q & 1);
+      read_frags((q + 1) & 1, 0, a0, b0);
+      mfmas(a1, b1);
+      // per group of NMF / NRD MFMAs: one fragment read; LDS-DMA pieces (2 * PPW) spread evenly
+#pragma unroll
+      for (int t = 0; t < NRD; ++t) {
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+        if (t < 2 * PPW) __builtin_amdgcn_sched_group_barrier(SG_VMR, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(SG_MFMA, NMF / NRD - 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(SG_MFMA, NMF % NRD, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    advance();
+
+    if ((q + 1) % nk != 0) continue;
+    // ---- epilogue of tile q / nk, straight from the accumulators: lane (li, g) of fragment
+    // (i, j) holds C[row0 + i*16 + li][col0 + j*16 + 4g + r], r = 0..3
+    int tm, tn;
+    tile_rc(off + (q / nk) * G, tiles_m, tiles_n, tm, tn);
+    const int64_t row0 = (int64_t)tm * BM + wr * 128 + li;
+    const int64_t col0 = (int64_t)tn * BM + wc * WCOLS + 4 * g;
+    const TC* R = reinterpret_cast<const TC*>(epi.resid);
+    TC* X = reinterpret_cast<TC*>(epi.aux);
+    const bool interior = (int64_t)tm * BM + BM <= M && (int64_t)tn * BM + BM <= N;
+    // loads first (bias, the first residual row), then a store stream with no wait in it: the
+    // residual rows are prefetched one ahead, so their waits only cover the previous row's stores.
+    // Interior tiles take a branch-free copy (no per-store exec branches, whose joins make the
+    // compiler drain every outstanding store before each block).
+    auto epilogue = [&](auto edge_t) {
+      constexpr bool EDGE = decltype(edge_t)::value;
+      const bool bias_c = epi.bias && epi.bias_mode == 1, bias_r = epi.bias && epi.bias_mode == 2;
+      float bc[NI][4], brw[8];
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bc[j][r] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) brw[i] = 0.f;
+      if (bias_c) {  // one uniform branch around straight-line loads (clamped: tail columns never stored)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t col = col0 + j * 16 + r;
+            bc[j][r] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
+          }
+      }
+      if (bias_r) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int64_t row = row0 + i * 16;
+          brw[i] = epi.bias[EDGE ? (row < M ? row : M - 1) : row];
+        }
+      }
+      float rc[NI][4], rn[NI][4];
+      auto load_resid = [&](int i, float (&rv)[NI][4]) {
+        const int64_t row = row0 + i * 16;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int64_t col = col0 + j * 16;
+          if (!EDGE || (row < M && col < N)) load4(R + row * epi.ldr + col, rv[j]);
+        }
+      };
+      if constexpr (HASR) load_resid(0, rc);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (HASR) {
+          if (i + 1 < 8) load_resid(i + 1, rn);
+        }
+        const int64_t row = row0 + i * 16;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int64_t col = col0 + j * 16;
+          if (!EDGE || (row < M && col < N)) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = epi.alpha * acc[i][j][r] + bc[j][r] + brw[i];
+            if (X) store4(X + row * epi.ldaux + col, v);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = apply_act(ACT, v[r]);
+            if constexpr (HASR) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += epi.beta * rc[j][r];
+            }
+            store4(C + row * ldc + col, v);
+          }
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if constexpr (HASR) {
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rc[j][r] = rn[j][r];
+        }
+      }
+    };
+    if (interior) epilogue(std::false_type{});
+    else epilogue(std::true_type{});
+    // interior: every VMEM op this epilogue issued came after the LDS-DMA of k-tile q+2 and their
+    // count is fixed, so the next barrier wait leaves them in flight
+    pend = interior ? 1 : 0;
+  }
+}
+}  // namespace w4
+
+int g_num_cus = 0;
+int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+      g_num_cus = n;
+    else
+      g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+
+// Eligible: bf16 k-contiguous A / B (16-B aligned rows), K % 64 == 0, one batch, no split, output /
+// residual / aux rows allow 4-column vector access, N a multiple of 4 and a 256-column tile
+// wasting <= 15 % of the columns, enough rows to fill the chip.
+bool pp_ok(const comet_gemm_args& a) {
+  if (getenv("COMET_GEMM_NO_PP") != nullptr) return false;
+  if (a.dtype_ab != COMET_BF16 || a.convert_a || a.convert_b || a.layout_a != 0 || a.layout_b != 0) return false;
+  if (a.batch[0] * a.batch[1] != 1 || a.k % 64 != 0 || a.k == 0 || a.split_k > 1) return false;
+  if ((uintptr_t)a.a % 16 != 0 || (uintptr_t)a.b % 16 != 0 || a.lda % 8 != 0 || a.ldb % 8 != 0) return false;
+  if (a.m < 4096 || a.n < 256 || a.n % 4 != 0 || a.m >= (1ll << 31) || a.n >= (1ll << 31)) return false;
+  if (a.lda * 256 + 64 >= (1ll << 31) || a.ldb * 256 + 64 >= (1ll << 31)) return false;  // 32-bit offsets
+  // in-step per-shape profile (tools/gemm_shapes.py): its 8-byte-per-lane stores lose to the parked
+  // 16-B row stores of the 256-row kernel once a second output (aux) or a residual read is fused
+  if ((a.aux != nullptr || a.resid != nullptr) && getenv("COMET_GEMM_PP_ALL_K") == nullptr) return false;
+  const int64_t w256 = cdiv(a.n, 256) * 256 - a.n;
+  if (w256 * 100 > 15 * a.n) return false;
+  const int es = a.dtype_c == COMET_F32 ? 4 : 2;
+  auto v4 = [&](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % (4 * es) == 0 && ld % 4 == 0); };
+  return v4(a.c, a.ldc) && v4(a.resid, a.ldr) && v4(a.aux, a.ldaux);
+}
+
+template <typename TC>
+int launch_pp(const comet_gemm_args& a, hipStream_t s) {
+  Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
+  const int64_t tiles_m = cdiv(a.m, w4::BM), tiles_n = cdiv(a.n, w4::BM);
+  COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 30), "comet_gemm: too many tiles");
+  const int ntiles = (int)(tiles_m * tiles_n);
+  int grid = num_cus();
+  grid -= grid % 8;
+  if (ntiles <= grid) grid = ntiles;
+#define PPK(ACT, HR)                                                                                          \
+  hipLaunchKernelGGL((w4::gemm_w4_kernel<TC, ACT, HR, 8>), dim3((unsigned)grid), dim3(512), 0, s,             \
+                     (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, a.n, a.k,     \
+                     (int)tiles_n, ntiles, e)
+#define PPR(ACT) do { if (a.resid) PPK(ACT, true); else PPK(ACT, false); } while (0)
+  switch (a.act) {
+    case COMET_ACT_GELU: PPR(COMET_ACT_GELU); break;
+    case COMET_ACT_RELU: PPR(COMET_ACT_RELU); break;
+    case COMET_ACT_SIGMOID: PPR(COMET_ACT_SIGMOID); break;
+    default: PPR(COMET_ACT_NONE);
+  }
+#undef PPR
+#undef PPK
+  COMET_CHECK_LAUNCH("comet_gemm (persistent 256 x 256, 4 waves)");
+  return COMET_OK;
+}
+
 // 0: not eligible, else the column tile (256 or 128) wasting the fewest columns
 int big_bn(const comet_gemm_args& a) {
   if (getenv("COMET_GEMM_NO_BIG") != nullptr) return 0;
@@ -961,7 +1296,7 @@ int big_bn(const comet_gemm_args& a) {
 }
 
 struct Plan {
-  int kind;      // 0 skinny, 1 256-row tile, 2 128 x 128 tile
+  int kind;      // 0 skinny, 1 256-row tile, 2 128 x 128 tile, 3 persistent 256 x 256 ping-pong
   int bn;        // kind 1
   int splits;    // requested K splits (before the workspace check)
 };
@@ -1034,6 +1369,7 @@ int choose_splits(const comet_gemm_args& a) {
 
 Plan make_plan(const comet_gemm_args& a) {
   if (skinny_ok(a)) return Plan{0, 0, 1};
+  if (pp_ok(a)) return Plan{3, 256, 1};
   if (const int bn = big_bn(a)) {
     int sp = 1;
     if (a.split_k >= 1) {
@@ -1423,6 +1759,7 @@ extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   hipStream_t s = as_stream(stream);
   const Plan plan = make_plan(a);
   if (plan.kind == 0) return a.dtype_c == COMET_BF16 ? launch_skinny<__bf16>(a, s) : launch_skinny<float>(a, s);
+  if (plan.kind == 3) return a.dtype_c == COMET_BF16 ? launch_pp<__bf16>(a, s) : launch_pp<float>(a, s);
   if (plan.kind == 1) {
     int sp = plan.splits;
     if (sp > 1 && (a.workspace == nullptr || a.workspace_bytes < plan_workspace(a, plan))) sp = 1;

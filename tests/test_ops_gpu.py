@@ -474,6 +474,36 @@ def test_gemm_256_tile_path(mnk, epi):
         _close(out, pre + b.double() + 0.5 * r.double(), 1e-4, 1e-4 * math.sqrt(K), f"256 resid {mnk}")
 
 
+@pytest.mark.parametrize("mnk", [(20000, 3072, 192), (70001, 768, 64), (33000, 1152, 256), (4100, 1024, 1536)])
+@pytest.mark.parametrize("epi", ["plain_f32", "gelu_aux_bf16", "bias_resid_f32", "inplace_resid_f32"])
+def test_gemm_persistent_path(mnk, epi):
+    """Persistent ping-pong 256 x 256 kernel: several tiles per workgroup (k-tile prefetch across
+    tile boundaries), M / N tails, every epilogue incl. an in-place residual (out is resid), vs f64."""
+    ops = _ops()
+    M, N, K = mnk
+    x = _rand(M, K, seed=94).to(torch.bfloat16)
+    w = _rand(N, K, seed=95, scale=0.1).to(torch.bfloat16)
+    b = _rand(N, seed=96)
+    pre = x.double() @ w.double().t()
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    if epi == "plain_f32":
+        out = ops.linear(xd, wd, out_dtype=torch.float32)
+        _close(out, pre, 1e-4, 1e-4 * math.sqrt(K), f"pp plain {mnk}")
+    elif epi == "gelu_aux_bf16":
+        aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        out = ops.linear(xd, wd, bias=bd, act=1, aux=aux, out_dtype=torch.bfloat16)
+        _close(aux, pre + b.double(), 1e-2, 1e-2, f"pp aux {mnk}")
+        _close(out, F.gelu(pre + b.double()), 1e-2, 1e-2, f"pp gelu {mnk}")
+    else:
+        r = _rand(M, N, seed=97)
+        rd = r.to(DEV)
+        if epi == "inplace_resid_f32":
+            out = ops.linear(xd, wd, bias=bd, resid=rd, beta=0.5, out=rd, out_dtype=torch.float32)
+        else:
+            out = ops.linear(xd, wd, bias=bd, resid=rd, beta=0.5, out_dtype=torch.float32)
+        _close(out, pre + b.double() + 0.5 * r.double(), 1e-4, 1e-4 * math.sqrt(K), f"pp resid {mnk}")
+
+
 @pytest.mark.parametrize("la,lb", [(0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("mnk", [(4096, 512, 128), (768, 3072, 20480), (1000, 1000, 640), (384, 1152, 8192)])
 def test_gemm_256_tile_transposed_and_split(la, lb, mnk):
