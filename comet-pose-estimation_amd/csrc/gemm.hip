@@ -1247,7 +1247,7 @@ bool pp_ok(const comet_gemm_args& a) {
   // 16-B row stores of the 256-row kernel once a second output (aux) or a residual read is fused
   if ((a.aux != nullptr || a.resid != nullptr) && getenv("COMET_GEMM_PP_ALL_K") == nullptr) return false;
   const int64_t w256 = cdiv(a.n, 256) * 256 - a.n;
-  if (w256 * 100 > 15 * a.n) return false;
+  if (w256 * 100 > 15 * a.n && getenv("COMET_GEMM_PP_ANY_N") == nullptr) return false;
   const int es = a.dtype_c == COMET_F32 ? 4 : 2;
   auto v4 = [&](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % (4 * es) == 0 && ld % 4 == 0); };
   return v4(a.c, a.ldc) && v4(a.resid, a.ldr) && v4(a.aux, a.ldaux);

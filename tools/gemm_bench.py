@@ -26,6 +26,9 @@ SHAPES = [  # (M, N, K, act, out dtype, resid)
     (65536, 384, 1536, 0, torch.float32, True),
     (65536, 256, 1024, 0, torch.float32, True),
     (65536, 768, 384, 0, torch.bfloat16, False),
+    (8192, 384, 1536, 0, torch.float32, True),
+    (8192, 384, 384, 0, torch.float32, True),
+    (74368, 768, 768, 0, torch.float32, True),
     (8192, 8192, 8192, 0, torch.bfloat16, False),
 ]
 
