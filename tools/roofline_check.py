@@ -19,7 +19,8 @@ import kname  # noqa: E402
 
 def main():
     bench = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-    nsteps = int(sys.argv[3]) if len(sys.argv) > 3 else bench["steps"] + bench["warmup"]
+    # bench.py runs warmup + an unprofiled and a profiled pass of `steps` each
+    nsteps = int(sys.argv[3]) if len(sys.argv) > 3 else 2 * bench["steps"] + bench["warmup"]
     rp = defaultdict(lambda: [0, 0.0])
     for r in csv.DictReader(open(sys.argv[2])):
         inst = kname.instance(r["Name"])
