@@ -990,7 +990,15 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   constexpr int PPW = 32 / NW;      // LDS-DMA pieces per operand per wave and k-tile (4 or 8)
   constexpr int NMF = 8 * NI;       // MFMAs per k-step (32 or 64)
   constexpr int NRD = 8 + NI;       // fragment reads per k-step (12 or 16)
-  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF];
+  // f32 outputs park each 16-row block in LDS and store whole 128-B lines (the direct 4-column
+  // f32 stores ran at half speed); bf16 outputs store straight from the accumulators
+  constexpr bool PARK = std::is_same<TC, float>::value;
+  constexpr int PPITCH = WCOLS;  // parked f32 row pitch; 16-B chunk c of row r at c ^ pswz(r)
+  constexpr int PARK_F = PARK ? NW * 16 * PPITCH : 0;  // f32 elements of the park region
+  // pswz: the 8 rows one ds_write_b128 lane group writes hit 8 distinct chunks, and the 4
+  // (row, 4-chunk) quads of each ds_read_b128 lane group of the row-contiguous re-read are disjoint
+  auto pswz = [](int r) { return (r & 7) | ((r & 2) << 2); };
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + 2 * PARK_F];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / WN, wc = wid % WN;
@@ -1099,9 +1107,11 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // an interior tile's epilogue its stores (all issued after that LDS-DMA) stay in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (pend) {
-      constexpr int E = 8 * NI * (1 + (HASR ? 1 : 0)) + 8 * NI;  // C stores (+ resid loads) (+ aux stores)
+      // VMEM ops per output kind of one epilogue: direct 8 x NI, parked 16 x (WCOLS / (8 * CPL))
+      constexpr int PER = PARK ? 16 * (WCOLS / (8 * (16 / (int)sizeof(TC)))) : 8 * NI;
+      constexpr int E = PER * (1 + (HASR ? 1 : 0)) + PER;  // C stores (+ resid loads) (+ aux stores)
       if (epi.aux) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E > 63 ? 63 : E) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E - 8 * NI > 63 ? 63 : E - 8 * NI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E - PER > 63 ? 63 : E - PER) : "memory");
       pend = 0;
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1112,6 +1122,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // ---- k-step 1: MFMAs on (a1, b1); LDS-DMA of k-tile q+2 into buffer q&1 (past the end of the
     // stream: a re-load of the last k-tile that nothing reads); reads of k-tile q+1's k-step-0
     // fragments (a0, b0) from buffer (q+1)&1 (garbage past the end, never used). Branch-free.
+    const bool tile_end = (q + 1) % nk == 0;
     {
       issue_cur(q & 1);
       read_frags((q + 1) & 1, 0, a0, b0);
@@ -1130,7 +1141,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     __builtin_amdgcn_sched_barrier(0);
     advance();
 
-    if ((q + 1) % nk != 0) continue;
+    if (!tile_end) continue;
     // ---- epilogue of tile q / nk, straight from the accumulators: lane (li, g) of fragment
     // (i, j) holds C[row0 + i*16 + li][col0 + j*16 + 4g + r], r = 0..3
     int tm, tn;
@@ -1146,14 +1157,12 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // compiler drain every outstanding store before each block).
     auto epilogue = [&](auto edge_t) {
       constexpr bool EDGE = decltype(edge_t)::value;
-      const bool bias_c = epi.bias && epi.bias_mode == 1, bias_r = epi.bias && epi.bias_mode == 2;
-      float bc[NI][4], brw[8];
+      const bool bias_c = epi.bias != nullptr;  // per-column bias only (pp_ok)
+      float bc[NI][4];
 #pragma unroll
       for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) bc[j][r] = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) brw[i] = 0.f;
       if (bias_c) {  // one uniform branch around straight-line loads (clamped: tail columns never stored)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
@@ -1162,13 +1171,6 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
             const int64_t col = col0 + j * 16 + r;
             bc[j][r] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
           }
-      }
-      if (bias_r) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int64_t row = row0 + i * 16;
-          brw[i] = epi.bias[EDGE ? (row < M ? row : M - 1) : row];
-        }
       }
       float rc[NI][4], rn[NI][4];
       auto load_resid = [&](int i, float (&rv)[NI][4]) {
@@ -1192,7 +1194,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
           if (!EDGE || (row < M && col < N)) {
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = epi.alpha * acc[i][j][r] + bc[j][r] + brw[i];
+            for (int r = 0; r < 4; ++r) v[r] = epi.alpha * acc[i][j][r] + bc[j][r];
             if (X) store4(X + row * epi.ldaux + col, v);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = apply_act(ACT, v[r]);
@@ -1212,8 +1214,88 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
         }
       }
     };
+    if constexpr (PARK) {
+      // parked epilogue: per 16-row block the wave parks its 16 x WCOLS raw accumulators in its own
+      // LDS slab (no barrier: only this wave touches it) and re-reads them row-contiguously, so
+      // every store / residual load instruction covers 8 rows x 128 B (whole lines)
+      constexpr int CPL = 16 / (int)sizeof(TC);       // output columns per lane per access (16 B)
+      constexpr int NTC = WCOLS / (8 * CPL);          // column passes per row (f32: 2, bf16: 1)
+      float* park = reinterpret_cast<float*>(smem + 2 * BUF) + wid * 16 * PPITCH;
+      const int rr = lane >> 3, cc = lane & 7;
+      const int64_t prow0 = (int64_t)tm * BM + wr * 128 + rr;           // + i*16 + h*8
+      const int64_t pcol0 = (int64_t)tn * BM + wc * WCOLS + cc * CPL;   // + t*8*CPL
+      auto pepilogue = [&](auto edge_t) {
+        constexpr bool EDGE = decltype(edge_t)::value;
+        const bool bias_c = epi.bias != nullptr;  // per-column bias only (pp_ok)
+        float bcp[NTC][CPL];
+#pragma unroll
+        for (int t = 0; t < NTC; ++t)
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) bcp[t][e] = 0.f;
+        if (bias_c) {
+#pragma unroll
+          for (int t = 0; t < NTC; ++t)
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) {
+              const int64_t col = pcol0 + t * 8 * CPL + e;
+              bcp[t][e] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
+            }
+        }
+        float rc[2][NTC][CPL];
+        auto load_resid = [&](int i, float (&rv)[2][NTC][CPL]) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int t = 0; t < NTC; ++t) {
+              const int64_t row = prow0 + i * 16 + h * 8, col = pcol0 + t * 8 * CPL;
+              if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, rv[h][t]);
+            }
+        };
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          // (a one-block-ahead residual prefetch spills at 256 VGPRs; the wait below covers the
+          // previous block's stores)
+          if constexpr (HASR) load_resid(i, rc);
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            *reinterpret_cast<f32x4*>(park + li * PPITCH + (((j * 4 + g) ^ pswz(li)) << 2)) = acc[i][j];
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int t = 0; t < NTC; ++t) {
+              const int64_t row = prow0 + i * 16 + h * 8, col = pcol0 + t * 8 * CPL;
+              float v[CPL];
+#pragma unroll
+              for (int e = 0; e < CPL; e += 4) {
+                const int prl = rr + h * 8, lc = (t * 8 * CPL + cc * CPL + e) >> 2;
+                const f32x4 p4 = *reinterpret_cast<const f32x4*>(park + prl * PPITCH + ((lc ^ pswz(prl)) << 2));
+                v[e] = p4[0]; v[e + 1] = p4[1]; v[e + 2] = p4[2]; v[e + 3] = p4[3];
+              }
+              if (!EDGE || (row < M && col < N)) {
+#pragma unroll
+                for (int e = 0; e < CPL; ++e) v[e] = epi.alpha * v[e] + bcp[t][e];
+                if (X) storen<CPL>(X + row * epi.ldaux + col, v);
+#pragma unroll
+                for (int e = 0; e < CPL; ++e) v[e] = apply_act(ACT, v[e]);
+                if constexpr (HASR) {
+#pragma unroll
+                  for (int e = 0; e < CPL; ++e) v[e] += epi.beta * rc[h][t][e];
+                }
+                storen<CPL>(C + row * ldc + col, v);
+              }
+            }
+          asm volatile("" ::: "memory");
+        }
+      };
+      if (interior) pepilogue(std::false_type{});
+      else pepilogue(std::true_type{});
+    } else {
     if (interior) epilogue(std::false_type{});
     else epilogue(std::true_type{});
+    }
     // interior: every VMEM op this epilogue issued came after the LDS-DMA of k-tile q+2 and their
     // count is fixed, so the next barrier wait leaves them in flight
     pend = interior ? 1 : 0;
@@ -1240,12 +1322,13 @@ bool pp_ok(const comet_gemm_args& a) {
   if (getenv("COMET_GEMM_NO_PP") != nullptr) return false;
   if (a.dtype_ab != COMET_BF16 || a.convert_a || a.convert_b || a.layout_a != 0 || a.layout_b != 0) return false;
   if (a.batch[0] * a.batch[1] != 1 || a.k % 64 != 0 || a.k == 0 || a.split_k > 1) return false;
+  if (a.bias && a.bias_mode != 1) return false;
   if ((uintptr_t)a.a % 16 != 0 || (uintptr_t)a.b % 16 != 0 || a.lda % 8 != 0 || a.ldb % 8 != 0) return false;
   if (a.m < 4096 || a.n < 256 || a.n % 4 != 0 || a.m >= (1ll << 31) || a.n >= (1ll << 31)) return false;
   if (a.lda * 256 + 64 >= (1ll << 31) || a.ldb * 256 + 64 >= (1ll << 31)) return false;  // 32-bit offsets
-  // in-step per-shape profile (tools/gemm_shapes.py): its 8-byte-per-lane stores lose to the parked
-  // 16-B row stores of the 256-row kernel once a second output (aux) or a residual read is fused
-  if ((a.aux != nullptr || a.resid != nullptr) && getenv("COMET_GEMM_PP_ALL_K") == nullptr) return false;
+  // in-step per-shape profile (tools/gemm_shapes.py): with a second (aux) output its direct
+  // 8-byte-per-lane bf16 stores lose to the parked 16-B row stores of the 256-row kernel
+  if (a.aux != nullptr && getenv("COMET_GEMM_PP_ALL_K") == nullptr) return false;
   const int64_t w256 = cdiv(a.n, 256) * 256 - a.n;
   if (w256 * 100 > 15 * a.n && getenv("COMET_GEMM_PP_ANY_N") == nullptr) return false;
   const int es = a.dtype_c == COMET_F32 ? 4 : 2;
