@@ -972,32 +972,36 @@ __device__ __forceinline__ void tile_rc(int L, int tiles_m, int tiles_n, int& tm
   tm = grp * WGM + rem % rows;
   tn = rem / rows;
 }
-constexpr int ASTAGE = BM * BK;  // bf16 elements of one operand image (32 KiB)
-constexpr int BUF = 2 * ASTAGE;  // A + B images of one k-tile (64 KiB)
 
 typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int SG_MFMA = 0x008, SG_DSR = 0x100, SG_VMR = 0x020;
 
-template <typename TC, int ACT, bool HASR, int NW>
+template <typename TC, int ACT, bool HASR, int NW, int TBM, int TBN>
 __global__ void __launch_bounds__(NW * 64, 1)
 gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, int ntiles,
                Epi epi) {
   constexpr int WN = NW / 2;        // wave grid 2 x WN
-  constexpr int WCOLS = BM / WN;    // wave tile columns (64 or 128)
-  constexpr int NI = WCOLS / 16;    // column fragments per wave (4 or 8)
-  constexpr int PPW = 32 / NW;      // LDS-DMA pieces per operand per wave and k-tile (4 or 8)
-  constexpr int NMF = 8 * NI;       // MFMAs per k-step (32 or 64)
-  constexpr int NRD = 8 + NI;       // fragment reads per k-step (12 or 16)
-  // f32 outputs park each 16-row block in LDS and store whole 128-B lines (the direct 4-column
-  // f32 stores ran at half speed); bf16 outputs store straight from the accumulators
+  constexpr int WROWS = TBM / 2;    // wave tile rows (128 or 64)
+  constexpr int WCOLS = TBN / WN;   // wave tile columns (64 or 96)
+  constexpr int MI = WROWS / 16;    // row fragments per wave
+  constexpr int NI = WCOLS / 16;    // column fragments per wave
+  constexpr int ASTAGE = TBM * BK;  // bf16 elements of the A image of one k-tile
+  constexpr int BUF = (TBM + TBN) * BK;  // A + B images of one k-tile (64 KiB)
+  constexpr int PA = TBM / 8 / NW, PB = TBN / 8 / NW;  // LDS-DMA pieces per wave and k-tile
+  constexpr int NMF = MI * NI;      // MFMAs per k-step
+  constexpr int NRD = MI + NI;      // fragment reads per k-step
+  // f32 outputs park each 8-row half block in LDS and store whole 128-B lines (the direct
+  // 4-column f32 stores ran at half speed); bf16 outputs store straight from the accumulators
   constexpr bool PARK = std::is_same<TC, float>::value;
-  constexpr int PPITCH = WCOLS;  // parked f32 row pitch; 16-B chunk c of row r at c ^ pswz(r)
-  constexpr int PARK_F = PARK ? NW * 16 * PPITCH : 0;  // f32 elements of the park region
-  // pswz: the 8 rows one ds_write_b128 lane group writes hit 8 distinct chunks, and the 4
-  // (row, 4-chunk) quads of each ds_read_b128 lane group of the row-contiguous re-read are disjoint
-  auto pswz = [](int r) { return (r & 7) | ((r & 2) << 2); };
+  // parked f32 row pitch: 64-wide slabs XOR-swizzle their 16-B chunks (c ^ pswz(r): the 8 rows
+  // one ds_write_b128 lane group writes hit 8 distinct chunks and the 4 (row, 4-chunk) quads of
+  // each ds_read_b128 lane group of the re-read are disjoint); 96-wide slabs pad rows to 100
+  constexpr bool PSWZ = (WCOLS & (WCOLS - 1)) == 0;
+  constexpr int PPITCH = PSWZ ? WCOLS : WCOLS + 4;
+  constexpr int PARK_F = PARK ? NW * 8 * PPITCH : 0;  // f32 elements of the park region
+  auto pswz = [](int r) { return PSWZ ? ((r & 7) | ((r & 2) << 2)) : 0; };
   __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + 2 * PARK_F];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1012,10 +1016,10 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   const int T = my_tiles * nk;
   if (T == 0) return;
 
-  // ---- load stream: a wave issues LDS-DMA pieces wid*PPW + p of each operand image (8 rows x 64 k
+  // ---- load stream: a wave issues LDS-DMA pieces wid*PA + p (A) and wid*PB + p (B) of the images (8 rows x 64 k
   // = 1 KiB each; 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)); source rows clamped (tails
   // re-read the last row, never stored)
-  const int prow = wid * PPW * 8 + (lane >> 3);                 // + p * 8
+  const int prowa = wid * PA * 8 + (lane >> 3), prowb = wid * PB * 8 + (lane >> 3);  // + p * 8
   const int lch0 = ((lane & 7) ^ ((lane >> 4) & 3)) * 8;        // chunk column, even p
   const int lch1 = ((lane & 7) ^ (4 | ((lane >> 4) & 3))) * 8;  // odd p
   // load-stream state: the k-tile the next issue_cur() loads (tile ld_it of this workgroup, k-tile
@@ -1023,28 +1027,30 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   int ld_it = 0, ld_kt = 0;
   const __bf16* ldA = A;
   const __bf16* ldB = B;
-  int offA[PPW], offB[PPW];
+  int offA[PA], offB[PB];
   auto set_load_tile = [&](int it) {
     int tm, tn;
     tile_rc(off + it * G, tiles_m, tiles_n, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BM;
+    const int m0 = tm * TBM, n0 = tn * TBN;
     ldA = A + (int64_t)m0 * lda;
     ldB = B + (int64_t)n0 * ldb;
 #pragma unroll
-    for (int p = 0; p < PPW; ++p) {
-      const int r = prow + p * 8, lch = (p & 1) ? lch1 : lch0;
-      offA[p] = (min(m0 + r, (int)M - 1) - m0) * (int)lda + lch;
-      offB[p] = (min(n0 + r, (int)N - 1) - n0) * (int)ldb + lch;
-    }
+    for (int p = 0; p < PA; ++p)
+      offA[p] = (min(m0 + prowa + p * 8, (int)M - 1) - m0) * (int)lda + ((p & 1) ? lch1 : lch0);
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      offB[p] = (min(n0 + prowb + p * 8, (int)N - 1) - n0) * (int)ldb + ((p & 1) ? lch1 : lch0);
   };
   auto issue_cur = [&](int buf) {
     const __bf16* pa = ldA + ld_kt * BK;
     const __bf16* pb = ldB + ld_kt * BK;
 #pragma unroll
-    for (int p = 0; p < PPW; ++p) {
-      __bf16* img = smem + buf * BUF + (wid * PPW + p) * 512;
-      __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)img, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]), (lds_void*)(img + ASTAGE), 16, 0, 0);
+    for (int p = 0; p < (PA > PB ? PA : PB); ++p) {
+      if (p < PA)
+        __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + buf * BUF + (wid * PA + p) * 512), 16, 0, 0);
+      if (p < PB)
+        __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]),
+                                         (lds_void*)(smem + buf * BUF + ASTAGE + (wid * PB + p) * 512), 16, 0, 0);
     }
   };
   // past the last k-tile the stream keeps re-loading it (into a buffer nothing reads again)
@@ -1055,23 +1061,23 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     }
   };
 
-  bf16x8 a0[8], b0[NI], a1[8], b1[NI];
-  auto read_frags = [&](int buf, int s, bf16x8 (&af)[8], bf16x8 (&bf)[NI]) {
+  bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
+  auto read_frags = [&](int buf, int s, bf16x8 (&af)[MI], bf16x8 (&bf)[NI]) {
     const __bf16* img = smem + buf * BUF;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = big::frag(img, wr * 128 + i * 16 + li, 4 * s + g);
+    for (int i = 0; i < MI; ++i) af[i] = big::frag(img, wr * WROWS + i * 16 + li, 4 * s + g);
 #pragma unroll
     for (int j = 0; j < NI; ++j) bf[j] = big::frag(img + ASTAGE, wc * WCOLS + j * 16 + li, 4 * s + g);
   };
 
-  f32x4 acc[8][NI];
+  f32x4 acc[MI][NI];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mfmas = [&](const bf16x8 (&af)[8], const bf16x8 (&bf)[NI]) {
+  auto mfmas = [&](const bf16x8 (&af)[MI], const bf16x8 (&bf)[NI]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
   };
@@ -1084,8 +1090,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   if (T > 1) {
     issue_cur(1);
     advance();
-    if constexpr (PPW == 8) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PA + PB) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -1107,8 +1112,8 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // an interior tile's epilogue its stores (all issued after that LDS-DMA) stay in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (pend) {
-      // VMEM ops per output kind of one epilogue: direct 8 x NI, parked 16 x (WCOLS / (8 * CPL))
-      constexpr int PER = PARK ? 16 * (WCOLS / (8 * (16 / (int)sizeof(TC)))) : 8 * NI;
+      // VMEM ops per output kind of one epilogue: direct MI x NI, parked 2 x MI x (WCOLS / (8 * CPL))
+      constexpr int PER = PARK ? 2 * MI * (WCOLS / (8 * (16 / (int)sizeof(TC)))) : MI * NI;
       constexpr int E = PER * (1 + (HASR ? 1 : 0)) + PER;  // C stores (+ resid loads) (+ aux stores)
       if (epi.aux) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E > 63 ? 63 : E) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E - PER > 63 ? 63 : E - PER) : "memory");
@@ -1127,11 +1132,11 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       issue_cur(q & 1);
       read_frags((q + 1) & 1, 0, a0, b0);
       mfmas(a1, b1);
-      // per group of NMF / NRD MFMAs: one fragment read; LDS-DMA pieces (2 * PPW) spread evenly
+      // per group of NMF / NRD MFMAs: one fragment read; LDS-DMA pieces (PA + PB) spread evenly
 #pragma unroll
       for (int t = 0; t < NRD; ++t) {
         __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
-        if (t < 2 * PPW) __builtin_amdgcn_sched_group_barrier(SG_VMR, 1, 0);
+        if (t < PA + PB) __builtin_amdgcn_sched_group_barrier(SG_VMR, 1, 0);
         __builtin_amdgcn_sched_group_barrier(SG_MFMA, 1, 0);
         __builtin_amdgcn_sched_group_barrier(SG_DSR, 1, 0);
         __builtin_amdgcn_sched_group_barrier(SG_MFMA, NMF / NRD - 2, 0);
@@ -1146,11 +1151,11 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // (i, j) holds C[row0 + i*16 + li][col0 + j*16 + 4g + r], r = 0..3
     int tm, tn;
     tile_rc(off + (q / nk) * G, tiles_m, tiles_n, tm, tn);
-    const int64_t row0 = (int64_t)tm * BM + wr * 128 + li;
-    const int64_t col0 = (int64_t)tn * BM + wc * WCOLS + 4 * g;
+    const int64_t row0 = (int64_t)tm * TBM + wr * WROWS + li;
+    const int64_t col0 = (int64_t)tn * TBN + wc * WCOLS + 4 * g;
     const TC* R = reinterpret_cast<const TC*>(epi.resid);
     TC* X = reinterpret_cast<TC*>(epi.aux);
-    const bool interior = (int64_t)tm * BM + BM <= M && (int64_t)tn * BM + BM <= N;
+    const bool interior = (int64_t)tm * TBM + TBM <= M && (int64_t)tn * TBN + TBN <= N;
     // loads first (bias, the first residual row), then a store stream with no wait in it: the
     // residual rows are prefetched one ahead, so their waits only cover the previous row's stores.
     // Interior tiles take a branch-free copy (no per-store exec branches, whose joins make the
@@ -1183,9 +1188,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       };
       if constexpr (HASR) load_resid(0, rc);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < MI; ++i) {
         if constexpr (HASR) {
-          if (i + 1 < 8) load_resid(i + 1, rn);
+          if (i + 1 < MI) load_resid(i + 1, rn);
         }
         const int64_t row = row0 + i * 16;
 #pragma unroll
@@ -1215,15 +1220,15 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       }
     };
     if constexpr (PARK) {
-      // parked epilogue: per 16-row block the wave parks its 16 x WCOLS raw accumulators in its own
-      // LDS slab (no barrier: only this wave touches it) and re-reads them row-contiguously, so
-      // every store / residual load instruction covers 8 rows x 128 B (whole lines)
+      // parked epilogue: per 8-row half of each 16-row block the wave parks its 8 x WCOLS raw
+      // accumulators in its own LDS slab (no barrier: only this wave touches it) and re-reads them
+      // row-contiguously, so every store / residual load instruction covers 8 rows x 128 B
       constexpr int CPL = 16 / (int)sizeof(TC);       // output columns per lane per access (16 B)
-      constexpr int NTC = WCOLS / (8 * CPL);          // column passes per row (f32: 2, bf16: 1)
-      float* park = reinterpret_cast<float*>(smem + 2 * BUF) + wid * 16 * PPITCH;
+      constexpr int NTC = WCOLS / (8 * CPL);          // column passes per row
+      float* park = reinterpret_cast<float*>(smem + 2 * BUF) + wid * 8 * PPITCH;
       const int rr = lane >> 3, cc = lane & 7;
-      const int64_t prow0 = (int64_t)tm * BM + wr * 128 + rr;           // + i*16 + h*8
-      const int64_t pcol0 = (int64_t)tn * BM + wc * WCOLS + cc * CPL;   // + t*8*CPL
+      const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;        // + i*16 + h*8
+      const int64_t pcol0 = (int64_t)tn * TBN + wc * WCOLS + cc * CPL;  // + t*8*CPL
       auto pepilogue = [&](auto edge_t) {
         constexpr bool EDGE = decltype(edge_t)::value;
         const bool bias_c = epi.bias != nullptr;  // per-column bias only (pp_ok)
@@ -1241,37 +1246,35 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
               bcp[t][e] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
             }
         }
-        float rc[2][NTC][CPL];
-        auto load_resid = [&](int i, float (&rv)[2][NTC][CPL]) {
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int t = 0; t < NTC; ++t) {
-              const int64_t row = prow0 + i * 16 + h * 8, col = pcol0 + t * 8 * CPL;
-              if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, rv[h][t]);
+          for (int h = 0; h < 2; ++h) {
+            // residual of these 8 rows first (its wait covers the previous half's stores; a
+            // prefetch one block ahead spills at 256 VGPRs)
+            float rc[NTC][CPL];
+            const int64_t row = prow0 + i * 16 + h * 8;
+            if constexpr (HASR) {
+#pragma unroll
+              for (int t = 0; t < NTC; ++t) {
+                const int64_t col = pcol0 + t * 8 * CPL;
+                if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, rc[t]);
+              }
             }
-        };
+            if ((li >> 3) == h) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          // (a one-block-ahead residual prefetch spills at 256 VGPRs; the wait below covers the
-          // previous block's stores)
-          if constexpr (HASR) load_resid(i, rc);
-#pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            *reinterpret_cast<f32x4*>(park + li * PPITCH + (((j * 4 + g) ^ pswz(li)) << 2)) = acc[i][j];
-            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
+              for (int j = 0; j < NI; ++j)
+                *reinterpret_cast<f32x4*>(park + (li & 7) * PPITCH + (((j * 4 + g) ^ pswz(li & 7)) << 2)) = acc[i][j];
+            }
+            asm volatile("" ::: "memory");
 #pragma unroll
             for (int t = 0; t < NTC; ++t) {
-              const int64_t row = prow0 + i * 16 + h * 8, col = pcol0 + t * 8 * CPL;
+              const int64_t col = pcol0 + t * 8 * CPL;
               float v[CPL];
 #pragma unroll
               for (int e = 0; e < CPL; e += 4) {
-                const int prl = rr + h * 8, lc = (t * 8 * CPL + cc * CPL + e) >> 2;
-                const f32x4 p4 = *reinterpret_cast<const f32x4*>(park + prl * PPITCH + ((lc ^ pswz(prl)) << 2));
+                const int lc = (t * 8 * CPL + cc * CPL + e) >> 2;
+                const f32x4 p4 = *reinterpret_cast<const f32x4*>(park + rr * PPITCH + ((lc ^ pswz(rr)) << 2));
                 v[e] = p4[0]; v[e + 1] = p4[1]; v[e + 2] = p4[2]; v[e + 3] = p4[3];
               }
               if (!EDGE || (row < M && col < N)) {
@@ -1282,13 +1285,17 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
                 for (int e = 0; e < CPL; ++e) v[e] = apply_act(ACT, v[e]);
                 if constexpr (HASR) {
 #pragma unroll
-                  for (int e = 0; e < CPL; ++e) v[e] += epi.beta * rc[h][t][e];
+                  for (int e = 0; e < CPL; ++e) v[e] += epi.beta * rc[t][e];
                 }
                 storen<CPL>(C + row * ldc + col, v);
               }
             }
-          asm volatile("" ::: "memory");
-        }
+            asm volatile("" ::: "memory");
+            if (h == 1) {
+#pragma unroll
+              for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
       };
       if (interior) pepilogue(std::false_type{});
       else pepilogue(std::true_type{});
@@ -1325,12 +1332,13 @@ bool pp_ok(const comet_gemm_args& a) {
   if (a.bias && a.bias_mode != 1) return false;
   if ((uintptr_t)a.a % 16 != 0 || (uintptr_t)a.b % 16 != 0 || a.lda % 8 != 0 || a.ldb % 8 != 0) return false;
   if (a.m < 4096 || a.n < 256 || a.n % 4 != 0 || a.m >= (1ll << 31) || a.n >= (1ll << 31)) return false;
-  if (a.lda * 256 + 64 >= (1ll << 31) || a.ldb * 256 + 64 >= (1ll << 31)) return false;  // 32-bit offsets
+  if (a.n == 384 && getenv("COMET_GEMM_NO_PP384") != nullptr) return false;
+  if (a.lda * 384 + 64 >= (1ll << 31) || a.ldb * 384 + 64 >= (1ll << 31)) return false;  // 32-bit offsets
   // in-step per-shape profile (tools/gemm_shapes.py): with a second (aux) output its direct
   // 8-byte-per-lane bf16 stores lose to the parked 16-B row stores of the 256-row kernel
   if (a.aux != nullptr && getenv("COMET_GEMM_PP_ALL_K") == nullptr) return false;
   const int64_t w256 = cdiv(a.n, 256) * 256 - a.n;
-  if (w256 * 100 > 15 * a.n && getenv("COMET_GEMM_PP_ANY_N") == nullptr) return false;
+  if (a.n != 384 && w256 * 100 > 15 * a.n && getenv("COMET_GEMM_PP_ANY_N") == nullptr) return false;
   const int es = a.dtype_c == COMET_F32 ? 4 : 2;
   auto v4 = [&](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % (4 * es) == 0 && ld % 4 == 0); };
   return v4(a.c, a.ldc) && v4(a.resid, a.ldr) && v4(a.aux, a.ldaux);
@@ -1339,16 +1347,21 @@ bool pp_ok(const comet_gemm_args& a) {
 template <typename TC>
 int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
-  const int64_t tiles_m = cdiv(a.m, w4::BM), tiles_n = cdiv(a.n, w4::BM);
+  // N = 384 (the tracker's hidden size): 128 x 384 tiles (each A row block read once);
+  // otherwise 256 x 256
+  const bool n384 = a.n == 384;
+  const int64_t tbm = n384 ? 128 : 256, tbn = n384 ? 384 : 256;
+  const int64_t tiles_m = cdiv(a.m, tbm), tiles_n = cdiv(a.n, tbn);
   COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 30), "comet_gemm: too many tiles");
   const int ntiles = (int)(tiles_m * tiles_n);
   int grid = num_cus();
   grid -= grid % 8;
   if (ntiles <= grid) grid = ntiles;
-#define PPK(ACT, HR)                                                                                          \
-  hipLaunchKernelGGL((w4::gemm_w4_kernel<TC, ACT, HR, 8>), dim3((unsigned)grid), dim3(512), 0, s,             \
+#define PPKT(ACT, HR, BMT, BNT)                                                                               \
+  hipLaunchKernelGGL((w4::gemm_w4_kernel<TC, ACT, HR, 8, BMT, BNT>), dim3((unsigned)grid), dim3(512), 0, s,   \
                      (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, a.n, a.k,     \
                      (int)tiles_n, ntiles, e)
+#define PPK(ACT, HR) do { if (n384) PPKT(ACT, HR, 128, 384); else PPKT(ACT, HR, 256, 256); } while (0)
 #define PPR(ACT) do { if (a.resid) PPK(ACT, true); else PPK(ACT, false); } while (0)
   switch (a.act) {
     case COMET_ACT_GELU: PPR(COMET_ACT_GELU); break;
@@ -1358,6 +1371,7 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   }
 #undef PPR
 #undef PPK
+#undef PPKT
   COMET_CHECK_LAUNCH("comet_gemm (persistent 256 x 256, 4 waves)");
   return COMET_OK;
 }

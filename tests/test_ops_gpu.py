@@ -474,11 +474,13 @@ def test_gemm_256_tile_path(mnk, epi):
         _close(out, pre + b.double() + 0.5 * r.double(), 1e-4, 1e-4 * math.sqrt(K), f"256 resid {mnk}")
 
 
-@pytest.mark.parametrize("mnk", [(20000, 3072, 192), (70001, 768, 64), (33000, 1152, 256), (4100, 1024, 1536)])
+@pytest.mark.parametrize("mnk", [(20000, 3072, 192), (70001, 768, 64), (33000, 1152, 256), (4100, 1024, 1536),
+                                 (20001, 384, 1536), (8200, 384, 384), (65536, 384, 64)])
 @pytest.mark.parametrize("epi", ["plain_f32", "gelu_aux_bf16", "bias_resid_f32", "inplace_resid_f32"])
 def test_gemm_persistent_path(mnk, epi):
-    """Persistent ping-pong 256 x 256 kernel: several tiles per workgroup (k-tile prefetch across
-    tile boundaries), M / N tails, every epilogue incl. an in-place residual (out is resid), vs f64."""
+    """Persistent kernel (256 x 256 tiles; 128 x 384 for N = 384): several tiles per workgroup
+    (k-tile prefetch across tile boundaries), M / N tails, direct (bf16) and parked (f32) epilogues
+    incl. an in-place residual (out is resid), vs f64."""
     ops = _ops()
     M, N, K = mnk
     x = _rand(M, K, seed=94).to(torch.bfloat16)
