@@ -118,7 +118,7 @@ def _plan_name(la, lb, cdt, odt, split):
     if kind == 1:
         return f"big{bn}.L{la}{lb}.{out}"
     if kind == 3:
-        return f"pp256.L{la}{lb}.{out}"
+        return f"pp{bn}.L{la}{lb}.{out}"
     return f"tile128.L{la}{lb}.{'bf16' if cdt == torch.bfloat16 else 'f32'}.{out}"
 
 

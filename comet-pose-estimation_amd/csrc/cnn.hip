@@ -1,3 +1,4 @@
+#include <cstdlib>
 // CNN operators on channels-last activations: im2col for the tracker encoders / DINOv2
 // patch-embed convolutions, and align_corners=True bilinear resize.
 //
@@ -103,6 +104,44 @@ resize_nhwc8_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n, int
   }
 }
 
+// Row-blocked variant (c % 8 == 0, 16-B aligned, n * oh < 2^31): output row (ni, oy) per
+// RowBlock row, its y interpolation computed once, 8 channels per item.
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+resize_nhwc8_rows_kernel(const TI* __restrict__ x, TO* __restrict__ y, RowBlock rb, int c, int h, int w,
+                         int oh, int ow, int add) {
+  const int rl = threadIdx.x / rb.R;
+  const int row = blockIdx.x * rb.RB + rl;
+  if (rl >= rb.RB || row >= rb.nrows) return;
+  const int ni = row / oh, oy = row - ni * oh;
+  int64_t y0, y1, x0, x1;
+  float fy, fx;
+  ac_coord(oy, h, oh, y0, y1, fy);
+  const int cg8 = c / 8;
+  const TI* b0 = x + ((int64_t)ni * h + y0) * w * c;
+  const TI* b1 = x + ((int64_t)ni * h + y1) * w * c;
+  TO* yrow = y + (int64_t)row * ow * c;
+  const int step = rb.R > 256 ? 256 : rb.R;
+  for (int it = threadIdx.x - rl * rb.R; it < rb.R; it += step) {
+    const int ox = it / cg8, cg = it - ox * cg8;
+    ac_coord(ox, w, ow, x0, x1, fx);
+    float v00[8], v01[8], v10[8], v11[8];
+    load8(b0 + x0 * c + cg * 8, v00);
+    load8(b0 + x1 * c + cg * 8, v01);
+    load8(b1 + x0 * c + cg * 8, v10);
+    load8(b1 + x1 * c + cg * 8, v11);
+    float o[8];
+    TO* yo = yrow + (int64_t)ox * c + cg * 8;
+    if (add) load8(yo, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (1.f - fy) * ((1.f - fx) * v00[e] + fx * v01[e]) + fy * ((1.f - fx) * v10[e] + fx * v11[e]);
+      o[e] = add ? o[e] + v : v;
+    }
+    store8(yo, o);
+  }
+}
+
 inline unsigned g1d(int64_t n) {
   int64_t g = cdiv(n, 256);
   return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
@@ -135,6 +174,19 @@ extern "C" int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, cons
                                      int64_t ow, int add, void* stream) {
   COMET_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "comet_resize_bilinear: bad args");
   hipStream_t s = as_stream(stream);
+  if (nhwc && c % 8 == 0 && ((uintptr_t)x | (uintptr_t)y) % 32 == 0 && n * oh < (1ll << 31) &&
+      ow * (c / 8) < (1ll << 24) && h < (1 << 30) && w < (1 << 30) && getenv("COMET_RESIZE_FLAT") == nullptr) {
+    const RowBlock rb = make_rowblock(n * oh, ow * (c / 8));
+    const unsigned gr = (unsigned)cdiv(rb.nrows, rb.RB);
+#define RSR(TI, TO) hipLaunchKernelGGL((resize_nhwc8_rows_kernel<TI, TO>), dim3(gr), dim3(256), 0, s, (const TI*)x, (TO*)y, rb, (int)c, (int)h, (int)w, (int)oh, (int)ow, add)
+    if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RSR(float, float);
+    else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) RSR(float, __bf16);
+    else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) RSR(__bf16, __bf16);
+    else RSR(__bf16, float);
+#undef RSR
+    COMET_CHECK_LAUNCH("comet_resize_bilinear");
+    return COMET_OK;
+  }
   if (nhwc && c % 8 == 0 && ((uintptr_t)x | (uintptr_t)y) % 32 == 0 && h < (1 << 30) && w < (1 << 30)) {
     const unsigned g8 = g1d(n * oh * ow * (c / 8));
 #define RS8(TI, TO) hipLaunchKernelGGL((resize_nhwc8_kernel<TI, TO>), dim3(g8), dim3(256), 0, s, (const TI*)x, (TO*)y, n, (int)c, (int)h, (int)w, (int)oh, (int)ow, add)

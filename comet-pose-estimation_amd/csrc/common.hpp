@@ -153,6 +153,21 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + local;
 }
 
+// Row-blocked NHWC launches (resize / pooling): R = items per output row (ow x channel groups),
+// a 256-thread block covers RB = max(1, 256 / R) output rows (n, oy) and loops over a row's items
+// when R > 256. Index math is 32-bit and done once per thread, not per element (the flat 64-bit
+// div / mod decomposition of a grid-stride loop made these kernels VALU-bound).
+struct RowBlock {
+  int R, RB, nrows;
+};
+inline RowBlock make_rowblock(int64_t nrows, int64_t items) {
+  RowBlock rb;
+  rb.R = (int)items;
+  rb.RB = items >= 256 ? 1 : (int)(256 / items);
+  rb.nrows = (int)nrows;
+  return rb;
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

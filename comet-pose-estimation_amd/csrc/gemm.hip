@@ -961,7 +961,7 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
 //    and the epilogue stores straight from the accumulators (no LDS park).
 // NW = 8: 2 x 4 waves of 128 x 64 (two waves per SIMD); NW = 4: 2 x 2 waves of 128 x 128.
 namespace w4 {
-constexpr int BM = 256, BK = 64;
+constexpr int BK = 64;
 constexpr int WGM = 8;  // logical tiles run down groups of WGM tile rows, column by column
 
 // logical tile -> (tile row, tile column): an XCD's 32 consecutive tiles form an 8 x 4 patch
@@ -1466,7 +1466,7 @@ int choose_splits(const comet_gemm_args& a) {
 
 Plan make_plan(const comet_gemm_args& a) {
   if (skinny_ok(a)) return Plan{0, 0, 1};
-  if (pp_ok(a)) return Plan{3, 256, 1};
+  if (pp_ok(a)) return Plan{3, a.n == 384 ? 384 : 256, 1};
   if (const int bn = big_bn(a)) {
     int sp = 1;
     if (a.split_k >= 1) {

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // Point-tracker kernels (coarse CoTracker-style predictor and fine refinement) + DINOv2 input
 // preparation. All feature maps are channels-last (NHWC).
 //
@@ -201,6 +202,33 @@ __global__ void avgpool2_kernel(const T* __restrict__ x, T* __restrict__ y, int6
     const T* base = x + ((b * H + 2 * oy) * W + 2 * ox) * C + c;
     const float s = to_f32(base[0]) + to_f32(base[C]) + to_f32(base[(int64_t)W * C]) + to_f32(base[(int64_t)W * C + C]);
     y[i] = from_f32<T>(s * 0.25f);
+  }
+}
+
+// Row-blocked, 8 channels (16 B of bf16 / 2 x 16 B of f32) per item (C % 8 == 0, aligned).
+template <typename T>
+__global__ void __launch_bounds__(256)
+avgpool2_rows_kernel(const T* __restrict__ x, T* __restrict__ y, RowBlock rb, int H, int W, int C) {
+  const int rl = threadIdx.x / rb.R;
+  const int row = blockIdx.x * rb.RB + rl;
+  if (rl >= rb.RB || row >= rb.nrows) return;
+  const int OH = H / 2, OW = W / 2, cg8 = C / 8;
+  const int b = row / OH, oy = row - b * OH;
+  const T* r0 = x + ((int64_t)b * H + 2 * oy) * W * C;
+  const T* r1 = r0 + (int64_t)W * C;
+  T* yrow = y + (int64_t)row * OW * C;
+  const int step = rb.R > 256 ? 256 : rb.R;
+  for (int it = threadIdx.x - rl * rb.R; it < rb.R; it += step) {
+    const int ox = it / cg8, cg = it - ox * cg8;
+    const int64_t o = (int64_t)(2 * ox) * C + cg * 8;
+    float a[8], bq[8], cq[8], d[8], out[8];
+    load8(r0 + o, a);
+    load8(r0 + o + C, bq);
+    load8(r1 + o, cq);
+    load8(r1 + o + C, d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[e] = (a[e] + bq[e] + cq[e] + d[e]) * 0.25f;
+    store8(yrow + (int64_t)ox * C + cg * 8, out);
   }
 }
 
@@ -475,6 +503,16 @@ extern "C" int comet_avgpool2_nhwc(int dtype, const void* x, void* y, int64_t n,
   COMET_CHECK_ARG(x && y && H >= 2 && W >= 2, "comet_avgpool2_nhwc: bad args");
   hipStream_t s = as_stream(stream);
   const int64_t tot = n * (H / 2) * (W / 2) * C;
+  if (C % 8 == 0 && ((uintptr_t)x | (uintptr_t)y) % 32 == 0 && n * (H / 2) < (1ll << 31) && getenv("COMET_POOL_FLAT") == nullptr) {
+    const RowBlock rb = make_rowblock(n * (H / 2), (int64_t)(W / 2) * (C / 8));
+    const unsigned gr = (unsigned)cdiv(rb.nrows, rb.RB);
+    if (dtype == COMET_F32)
+      hipLaunchKernelGGL((avgpool2_rows_kernel<float>), dim3(gr), dim3(256), 0, s, (const float*)x, (float*)y, rb, H, W, C);
+    else
+      hipLaunchKernelGGL((avgpool2_rows_kernel<__bf16>), dim3(gr), dim3(256), 0, s, (const __bf16*)x, (__bf16*)y, rb, H, W, C);
+    COMET_CHECK_LAUNCH("comet_avgpool2_nhwc");
+    return COMET_OK;
+  }
   if (dtype == COMET_F32)
     hipLaunchKernelGGL((avgpool2_kernel<float>), dim3(g1d(tot)), dim3(256), 0, s, (const float*)x, (float*)y, n, H, W, C);
   else

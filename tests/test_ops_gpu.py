@@ -309,6 +309,33 @@ def test_resize_nhwc_vector_add(dtype):
     _close(out.permute(0, 3, 1, 2), ref, tol, tol, f"resize nhwc add {dtype}")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,c,h,w,oh,ow", [(300, 32, 16, 16, 31, 31), (3, 416, 16, 16, 64, 64), (7, 8, 5, 3, 1, 1),
+                                           (2, 128, 64, 64, 32, 32)])
+def test_resize_nhwc_row_blocked(dtype, n, c, h, w, oh, ow):
+    """Row-blocked NHWC resize: several output rows per block (ow * c/8 < 256), one row looped over
+    (> 256 items), 1 x 1 output; vs ATen align_corners in f64."""
+    ops = _ops()
+    x = _rand(n, c, h, w, seed=34).to(dtype)
+    ref = F.interpolate(x.double(), (oh, ow), mode="bilinear", align_corners=True)
+    y = ops.resize_bilinear(x.permute(0, 2, 3, 1).contiguous().to(DEV), oh, ow, nhwc=True)
+    tol = 5e-5 if dtype == torch.float32 else 1.6e-2
+    _close(y.permute(0, 3, 1, 2), ref, tol, tol, f"resize rows {dtype} {(n, c, h, w, oh, ow)}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("n,c,h,w", [(300, 32, 31, 31), (4, 128, 64, 64), (2, 128, 5, 7), (3, 12, 8, 8)])
+def test_avgpool2_nhwc(dtype, n, c, h, w):
+    """2x2 average pool (CorrBlock pyramid, blocks.py:351-429: F.avg_pool2d(k=2, s=2), odd sizes
+    floor): row-blocked 8-channel path and the scalar path (c % 8 != 0)."""
+    ops = _ops()
+    x = _rand(n, c, h, w, seed=35).to(dtype)
+    ref = F.avg_pool2d(x.double(), 2, stride=2)
+    y = ops.avgpool2_nhwc(x.permute(0, 2, 3, 1).contiguous().to(DEV))
+    tol = 1e-6 if dtype == torch.float32 else 8e-3
+    _close(y.permute(0, 3, 1, 2), ref, tol, tol, f"avgpool2 {dtype} {(n, c, h, w)}")
+
+
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("which", ["a", "b", "ab"])
 @pytest.mark.parametrize("mnk", [(200, 136, 264), (96, 64, 6000)])
