@@ -392,6 +392,73 @@ __global__ void score_kernel(const float* __restrict__ qfeat, const TF* __restri
   }
 }
 
+// Parallel form of score_kernel (the per-track loop ran 4096 threads for the whole chip): one
+// thread per (b, s, n) window, channels 8 at a time (C % 8 == 0), then a per-track pass that
+// divides by the max inverse score over s. Same arithmetic and reads as score_kernel.
+template <typename TF>
+__global__ void __launch_bounds__(256)
+score_items_kernel(const float* __restrict__ qfeat, const TF* __restrict__ pfeat, const float* __restrict__ fine,
+                   float* __restrict__ score, float* __restrict__ inv_score, int B, int S, int N, int P, int C,
+                   int sradius) {
+  const int item = blockIdx.x * 256 + threadIdx.x;  // (b*S + s)*N + n
+  if (item >= B * S * N) return;
+  const int n = item % N, t = item / N, s = t % S, b = t / S;
+  float sc = 1.f;
+  if (s > 0) {
+    const int ss = 2 * sradius + 1;
+    const float lin_step = 2.f / (float)(ss - 1);
+    const float* q = qfeat + ((int64_t)b * N + n) * C;
+    const TF* fm = pfeat + ((int64_t)b * N * S) * P * P * C;
+    const int m = item;  // flat (b s n) position, read in (b n, s) order
+    const int bn2 = m / S, s2 = m - bn2 * S;
+    const float fx = fine[((int64_t)bn2 * S + s2) * 2], fy = fine[((int64_t)bn2 * S + s2) * 2 + 1];
+    int tx = (int)floorf(fx) - sradius, ty = (int)floorf(fy) - sradius;
+    const int lim = P - ss;
+    tx = tx < 0 ? 0 : (tx > lim ? lim : tx);
+    ty = ty < 0 ? 0 : (ty > lim ? lim : ty);
+    float sim[25];
+    float mx = -INFINITY;
+    const float rs = 1.f / sqrtf((float)C);
+    for (int a = 0; a < ss; ++a)
+      for (int c2 = 0; c2 < ss; ++c2) {
+        const TF* pix = fm + ((int64_t)(ty + a) * P + (tx + c2)) * C;
+        float d = 0.f;
+        for (int c = 0; c < C; c += 8) {
+          float pv[8], qv[8];
+          load8(pix + c, pv);
+          load8(q + c, qv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d += qv[e] * pv[e];
+        }
+        d *= rs;
+        sim[a * ss + c2] = d;
+        mx = fmaxf(mx, d);
+      }
+    float den = 0.f;
+    for (int k = 0; k < ss * ss; ++k) { sim[k] = expf(sim[k] - mx); den += sim[k]; }
+    float ex = 0.f, ey = 0.f, ex2 = 0.f, ey2 = 0.f;
+    for (int a = 0; a < ss; ++a)
+      for (int c2 = 0; c2 < ss; ++c2) {
+        const float p = sim[a * ss + c2] / den;
+        const float gx = -1.f + lin_step * (float)c2, gy = -1.f + lin_step * (float)a;
+        ex += p * gx; ey += p * gy; ex2 += p * gx * gx; ey2 += p * gy * gy;
+      }
+    sc = sqrtf(fmaxf(ex2 - ex * ex, 1e-10f)) + sqrtf(fmaxf(ey2 - ey * ey, 1e-10f));
+  }
+  score[item] = sc;
+  inv_score[item] = 1.f / (sc + 1e-6f);
+}
+
+__global__ void __launch_bounds__(256)
+score_norm_kernel(float* __restrict__ inv_score, int B, int S, int N) {
+  const int t = blockIdx.x * 256 + threadIdx.x;  // b*N + n
+  if (t >= B * N) return;
+  const int b = t / N, n = t - b * N;
+  float mx = 0.f;
+  for (int s = 0; s < S; ++s) mx = fmaxf(mx, inv_score[((int64_t)b * S + s) * N + n]);
+  for (int s = 0; s < S; ++s) inv_score[((int64_t)b * S + s) * N + n] /= mx;
+}
+
 // DINOv2 input: x [BS, 3, H, W] f32 -> bilinear(align_corners) to R x R -> (x - mean)/std ->
 // patch rows cols[(f*g + py)*g + px][ci*p*p + ky*p + kx] (conv weight flatten order), K padded.
 template <typename TO>
@@ -572,6 +639,19 @@ extern "C" int comet_track_score(int dtype_feat, const float* qfeat, const void*
   COMET_CHECK_ARG(sradius >= 1 && sradius <= 2 && P > 2 * sradius, "comet_track_score: sradius must be 1 or 2");
   if (B * N == 0) return COMET_OK;
   hipStream_t s = as_stream(stream);
+  if (C % 8 == 0 && (uintptr_t)pfeat % 16 == 0 && (uintptr_t)qfeat % 16 == 0 && B * S * N < (1ll << 31) &&
+      getenv("COMET_SCORE_SERIAL") == nullptr) {
+    const unsigned g = (unsigned)cdiv(B * S * N, 256), g2 = (unsigned)cdiv(B * N, 256);
+    if (dtype_feat == COMET_F32)
+      hipLaunchKernelGGL((score_items_kernel<float>), dim3(g), dim3(256), 0, s, qfeat, (const float*)pfeat, fine, score,
+                         inv_score, (int)B, S, (int)N, P, C, sradius);
+    else
+      hipLaunchKernelGGL((score_items_kernel<__bf16>), dim3(g), dim3(256), 0, s, qfeat, (const __bf16*)pfeat, fine, score,
+                         inv_score, (int)B, S, (int)N, P, C, sradius);
+    hipLaunchKernelGGL(score_norm_kernel, dim3(g2), dim3(256), 0, s, inv_score, (int)B, S, (int)N);
+    COMET_CHECK_LAUNCH("comet_track_score");
+    return COMET_OK;
+  }
   if (dtype_feat == COMET_F32)
     hipLaunchKernelGGL((score_kernel<float>), dim3(g1d(B * N)), dim3(256), 0, s, qfeat, (const float*)pfeat, fine, score, inv_score, B, S, N, P, C, sradius);
   else

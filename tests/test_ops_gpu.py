@@ -336,6 +336,24 @@ def test_avgpool2_nhwc(dtype, n, c, h, w):
     _close(y.permute(0, 3, 1, 2), ref, tol, tol, f"avgpool2 {dtype} {(n, c, h, w)}")
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,S,N", [(2, 5, 37), (1, 16, 64)])
+def test_track_score_parallel_matches_serial(dtype, B, S, N, monkeypatch):
+    """compute_score_fn (refine_track.py:174-278): the one-thread-per-window kernel equals the
+    per-track loop (whose parity with the reference is pinned end to end by the model goldens),
+    incl. windows clamped at the patch border."""
+    ops = _ops()
+    P, C = 31, 32
+    q = _rand(B * N, C, seed=36).to(DEV)
+    pf = _rand(B * N, S, P, P, C, seed=37).to(dtype).to(DEV)
+    fine = (torch.rand(B * N, S, 2, generator=torch.Generator().manual_seed(38)) * 34 - 2).to(DEV)
+    s1, i1 = ops.track_score(q, pf, fine, B, S, N)
+    monkeypatch.setenv("COMET_SCORE_SERIAL", "1")
+    s2, i2 = ops.track_score(q, pf, fine, B, S, N)
+    _close(s1, s2.double(), 1e-5, 1e-5, "score")
+    _close(i1, i2.double(), 1e-5, 1e-5, "inv score")
+
+
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("which", ["a", "b", "ab"])
 @pytest.mark.parametrize("mnk", [(200, 136, 264), (96, 64, 6000)])

@@ -3,6 +3,6 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/small
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -m gpu -x -q -k "resize or avgpool or instnorm" --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_ops_gpu.py -m gpu -x -q -k "resize or avgpool or instnorm or track_score" --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err
 echo done
