@@ -1020,8 +1020,6 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   // = 1 KiB each; 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)); source rows clamped (tails
   // re-read the last row, never stored)
   const int prowa = wid * PA * 8 + (lane >> 3), prowb = wid * PB * 8 + (lane >> 3);  // + p * 8
-  const int lch0 = ((lane & 7) ^ ((lane >> 4) & 3)) * 8;        // chunk column, even p
-  const int lch1 = ((lane & 7) ^ (4 | ((lane >> 4) & 3))) * 8;  // odd p
   // load-stream state: the k-tile the next issue_cur() loads (tile ld_it of this workgroup, k-tile
   // ld_kt of it); per tile, uniform row-block bases and per-lane 32-bit element offsets
   int ld_it = 0, ld_kt = 0;
@@ -1034,12 +1032,14 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     const int m0 = tm * TBM, n0 = tn * TBN;
     ldA = A + (int64_t)m0 * lda;
     ldB = B + (int64_t)n0 * ldb;
+    // chunk swizzle of image row r: c ^ ((r >> 1) & 7) (r = this lane's row in the image)
+    auto lch = [&](int r) { return ((lane & 7) ^ ((r >> 1) & 7)) * 8; };
 #pragma unroll
     for (int p = 0; p < PA; ++p)
-      offA[p] = (min(m0 + prowa + p * 8, (int)M - 1) - m0) * (int)lda + ((p & 1) ? lch1 : lch0);
+      offA[p] = (min(m0 + prowa + p * 8, (int)M - 1) - m0) * (int)lda + lch(prowa + p * 8);
 #pragma unroll
     for (int p = 0; p < PB; ++p)
-      offB[p] = (min(n0 + prowb + p * 8, (int)N - 1) - n0) * (int)ldb + ((p & 1) ? lch1 : lch0);
+      offB[p] = (min(n0 + prowb + p * 8, (int)N - 1) - n0) * (int)ldb + lch(prowb + p * 8);
   };
   auto issue_cur = [&](int buf) {
     const __bf16* pa = ldA + ld_kt * BK;
@@ -1350,18 +1350,26 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   // N = 384 (the tracker's hidden size): 128 x 384 tiles (each A row block read once);
   // otherwise 256 x 256
   const bool n384 = a.n == 384;
-  const int64_t tbm = n384 ? 128 : 256, tbn = n384 ? 384 : 256;
+  int grid = num_cus();
+  grid -= grid % 8;
+  // half-height tiles when the full-height ones leave CUs idle (M = 8192: the tracker's virtual
+  // tracks x frames x batch)
+  const int64_t tbn = n384 ? 384 : 256;
+  const bool half = cdiv(a.m, n384 ? 128 : 256) * cdiv(a.n, tbn) < grid;
+  const int64_t tbm = (n384 ? 128 : 256) / (half ? 2 : 1);
   const int64_t tiles_m = cdiv(a.m, tbm), tiles_n = cdiv(a.n, tbn);
   COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 30), "comet_gemm: too many tiles");
   const int ntiles = (int)(tiles_m * tiles_n);
-  int grid = num_cus();
-  grid -= grid % 8;
   if (ntiles <= grid) grid = ntiles;
 #define PPKT(ACT, HR, BMT, BNT)                                                                               \
   hipLaunchKernelGGL((w4::gemm_w4_kernel<TC, ACT, HR, 8, BMT, BNT>), dim3((unsigned)grid), dim3(512), 0, s,   \
                      (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, a.n, a.k,     \
                      (int)tiles_n, ntiles, e)
-#define PPK(ACT, HR) do { if (n384) PPKT(ACT, HR, 128, 384); else PPKT(ACT, HR, 256, 256); } while (0)
+#define PPK(ACT, HR)                                                                                          \
+  do {                                                                                                        \
+    if (n384) { if (half) PPKT(ACT, HR, 64, 384); else PPKT(ACT, HR, 128, 384); }                           \
+    else { if (half) PPKT(ACT, HR, 128, 256); else PPKT(ACT, HR, 256, 256); }                               \
+  } while (0)
 #define PPR(ACT) do { if (a.resid) PPK(ACT, true); else PPK(ACT, false); } while (0)
   switch (a.act) {
     case COMET_ACT_GELU: PPR(COMET_ACT_GELU); break;

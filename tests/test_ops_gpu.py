@@ -520,7 +520,8 @@ def test_gemm_256_tile_path(mnk, epi):
 
 
 @pytest.mark.parametrize("mnk", [(20000, 3072, 192), (70001, 768, 64), (33000, 1152, 256), (4100, 1024, 1536),
-                                 (20001, 384, 1536), (8200, 384, 384), (65536, 384, 64)])
+                                 (20001, 384, 1536), (8200, 384, 384), (65536, 384, 64),
+                                 (8192, 1536, 384), (6000, 768, 192)])
 @pytest.mark.parametrize("epi", ["plain_f32", "gelu_aux_bf16", "bias_resid_f32", "inplace_resid_f32"])
 def test_gemm_persistent_path(mnk, epi):
     """Persistent kernel (256 x 256 tiles; 128 x 384 for N = 384): several tiles per workgroup

@@ -28,6 +28,8 @@ SHAPES = [  # (M, N, K, act, out dtype, resid)
     (65536, 768, 384, 0, torch.bfloat16, False),
     (8192, 384, 1536, 0, torch.float32, True),
     (8192, 384, 384, 0, torch.float32, True),
+    (8192, 1536, 384, 1, torch.bfloat16, False),
+    (8192, 1152, 384, 0, torch.bfloat16, False),
     (74368, 768, 768, 0, torch.float32, True),
     (8192, 8192, 8192, 0, torch.bfloat16, False),
 ]
