@@ -117,8 +117,8 @@ def _plan_name(la, lb, cdt, odt, split):
         return f"skinny.{out}"
     if kind == 1:
         return f"big{bn}.L{la}{lb}.{out}"
-    if kind == 3:
-        return f"pp{bn}.L{la}{lb}.{out}"
+    if kind == 3:  # persistent tile kernel: _PLAN[2] = tile rows
+        return f"pp{_PLAN[2]}x{bn}.L{la}{lb}.{out}"
     return f"tile128.L{la}{lb}.{'bf16' if cdt == torch.bfloat16 else 'f32'}.{out}"
 
 

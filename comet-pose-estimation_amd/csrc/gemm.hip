@@ -1344,19 +1344,27 @@ bool pp_ok(const comet_gemm_args& a) {
   return v4(a.c, a.ldc) && v4(a.resid, a.ldr) && v4(a.aux, a.ldaux);
 }
 
+// Tile of the persistent kernel: 128 x 384 for N = 384 (the tracker's hidden size: each A row
+// block read once), else 256 x 256; half-height (64 x 384, 128 x 256) when the full-height tiles
+// leave CUs idle (M = 8192: the tracker's virtual tracks x frames x batch).
+void pp_tile(const comet_gemm_args& a, int& tbm, int& tbn) {
+  int cus = num_cus();
+  cus -= cus % 8;
+  tbn = a.n == 384 ? 384 : 256;
+  tbm = a.n == 384 ? 128 : 256;
+  if (cdiv(a.m, tbm) * cdiv(a.n, tbn) < cus) tbm /= 2;
+}
+
 template <typename TC>
 int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
   // N = 384 (the tracker's hidden size): 128 x 384 tiles (each A row block read once);
   // otherwise 256 x 256
-  const bool n384 = a.n == 384;
   int grid = num_cus();
   grid -= grid % 8;
-  // half-height tiles when the full-height ones leave CUs idle (M = 8192: the tracker's virtual
-  // tracks x frames x batch)
-  const int64_t tbn = n384 ? 384 : 256;
-  const bool half = cdiv(a.m, n384 ? 128 : 256) * cdiv(a.n, tbn) < grid;
-  const int64_t tbm = (n384 ? 128 : 256) / (half ? 2 : 1);
+  int tbm, tbn;
+  pp_tile(a, tbm, tbn);
+  const bool n384 = tbn == 384, half = tbm == (n384 ? 64 : 128);
   const int64_t tiles_m = cdiv(a.m, tbm), tiles_n = cdiv(a.n, tbn);
   COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 30), "comet_gemm: too many tiles");
   const int ntiles = (int)(tiles_m * tiles_n);
@@ -1401,9 +1409,10 @@ int big_bn(const comet_gemm_args& a) {
 }
 
 struct Plan {
-  int kind;      // 0 skinny, 1 256-row tile, 2 128 x 128 tile, 3 persistent 256 x 256 ping-pong
-  int bn;        // kind 1
+  int kind;      // 0 skinny, 1 256-row tile, 2 128 x 128 tile, 3 persistent tile kernel
+  int bn;        // kind 1, 3: column tile
   int splits;    // requested K splits (before the workspace check)
+  int bm = 0;    // kind 3: row tile
 };
 
 Plan make_plan(const comet_gemm_args& a);
@@ -1474,7 +1483,11 @@ int choose_splits(const comet_gemm_args& a) {
 
 Plan make_plan(const comet_gemm_args& a) {
   if (skinny_ok(a)) return Plan{0, 0, 1};
-  if (pp_ok(a)) return Plan{3, a.n == 384 ? 384 : 256, 1};
+  if (pp_ok(a)) {
+    int tbm, tbn;
+    pp_tile(a, tbm, tbn);
+    return Plan{3, tbn, 1, tbm};
+  }
   if (const int bn = big_bn(a)) {
     int sp = 1;
     if (a.split_k >= 1) {
@@ -1850,7 +1863,7 @@ extern "C" int comet_gemm_plan(const comet_gemm_args* args, int64_t* bytes, int3
   *bytes = plan_workspace(*args, p);
   plan[0] = p.kind;
   plan[1] = p.bn;
-  plan[2] = p.splits;
+  plan[2] = p.kind == 3 ? p.bm : p.splits;
   return COMET_OK;
 }
 
