@@ -52,8 +52,13 @@ class BasicEncoder(nn.Module):
         c = self.layer3(b)
         d = self.layer4(c)
         oh, ow = H // self.stride, W // self.stride
-        ups = [ops.resize_bilinear(t, oh, ow, nhwc=True) for t in (a, b, c, d)]
-        x = torch.cat(ups, dim=-1)
+        # the four up-sampled maps are written straight into their concat channel slices
+        parts = (a, b, c, d)
+        x = torch.empty(a.shape[0], oh, ow, sum(t.shape[-1] for t in parts), device=a.device, dtype=a.dtype)
+        c0 = 0
+        for t in parts:
+            ops.resize_bilinear_into(t, x[..., c0:c0 + t.shape[-1]])
+            c0 += t.shape[-1]
         x = ops.instnorm_nhwc(conv2d_nhwc(x, self.conv2, 1, 1), relu=True)
         return conv2d_nhwc(x, self.conv3, 1, 0)
 

@@ -425,6 +425,19 @@ def resize_bilinear(x, oh, ow, nhwc, out=None, add=False, out_dtype=None):
     return out
 
 
+def resize_bilinear_into(x, out, add=False):
+    """NHWC x [n, h, w, c] resized into out [n, oh, ow, c], a channel slice of a wider NHWC tensor
+    (out.stride() == (oh*ow*ld, ow*ld, ld, 1))."""
+    n, h, w, c = x.shape
+    on, oh, ow, oc = out.shape
+    ld = out.stride(2)
+    assert on == n and oc == c and out.stride(3) == 1 and out.stride(1) == ow * ld and out.stride(0) == oh * ow * ld
+    xc = x.contiguous()
+    L.check(L.load().comet_resize_bilinear_nhwc_into(dt(xc), dt(out), _p(xc), _p(out), n, c, h, w, oh, ow, ld,
+                                                     int(add), stream()), "resize_bilinear_into")
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # camera head helpers
 # ------------------------------------------------------------------------------------------

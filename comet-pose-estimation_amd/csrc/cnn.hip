@@ -109,7 +109,7 @@ resize_nhwc8_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n, int
 template <typename TI, typename TO>
 __global__ void __launch_bounds__(256)
 resize_nhwc8_rows_kernel(const TI* __restrict__ x, TO* __restrict__ y, RowBlock rb, int c, int h, int w,
-                         int oh, int ow, int add) {
+                         int oh, int ow, int add, int ldy) {
   const int rl = threadIdx.x / rb.R;
   const int row = blockIdx.x * rb.RB + rl;
   if (rl >= rb.RB || row >= rb.nrows) return;
@@ -120,7 +120,7 @@ resize_nhwc8_rows_kernel(const TI* __restrict__ x, TO* __restrict__ y, RowBlock 
   const int cg8 = c / 8;
   const TI* b0 = x + ((int64_t)ni * h + y0) * w * c;
   const TI* b1 = x + ((int64_t)ni * h + y1) * w * c;
-  TO* yrow = y + (int64_t)row * ow * c;
+  TO* yrow = y + (int64_t)row * ow * ldy;
   const int step = rb.R > 256 ? 256 : rb.R;
   for (int it = threadIdx.x - rl * rb.R; it < rb.R; it += step) {
     const int ox = it / cg8, cg = it - ox * cg8;
@@ -131,7 +131,7 @@ resize_nhwc8_rows_kernel(const TI* __restrict__ x, TO* __restrict__ y, RowBlock 
     load8(b1 + x0 * c + cg * 8, v10);
     load8(b1 + x1 * c + cg * 8, v11);
     float o[8];
-    TO* yo = yrow + (int64_t)ox * c + cg * 8;
+    TO* yo = yrow + (int64_t)ox * ldy + cg * 8;
     if (add) load8(yo, o);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -178,7 +178,7 @@ extern "C" int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, cons
       ow * (c / 8) < (1ll << 24) && h < (1 << 30) && w < (1 << 30) && getenv("COMET_RESIZE_FLAT") == nullptr) {
     const RowBlock rb = make_rowblock(n * oh, ow * (c / 8));
     const unsigned gr = (unsigned)cdiv(rb.nrows, rb.RB);
-#define RSR(TI, TO) hipLaunchKernelGGL((resize_nhwc8_rows_kernel<TI, TO>), dim3(gr), dim3(256), 0, s, (const TI*)x, (TO*)y, rb, (int)c, (int)h, (int)w, (int)oh, (int)ow, add)
+#define RSR(TI, TO) hipLaunchKernelGGL((resize_nhwc8_rows_kernel<TI, TO>), dim3(gr), dim3(256), 0, s, (const TI*)x, (TO*)y, rb, (int)c, (int)h, (int)w, (int)oh, (int)ow, add, (int)c)
     if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RSR(float, float);
     else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) RSR(float, __bf16);
     else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) RSR(__bf16, __bf16);
@@ -206,5 +206,26 @@ extern "C" int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, cons
   else RS(__bf16, float);
 #undef RS
   COMET_CHECK_LAUNCH("comet_resize_bilinear");
+  return COMET_OK;
+}
+
+extern "C" int comet_resize_bilinear_nhwc_into(int dtype_in, int dtype_out, const void* x, void* y, int64_t n,
+                                               int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
+                                               int64_t ldy, int add, void* stream) {
+  COMET_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "comet_resize_bilinear_nhwc_into: bad args");
+  COMET_CHECK_ARG(c % 8 == 0 && ldy % 8 == 0 && ldy >= c && ((uintptr_t)x | (uintptr_t)y) % 16 == 0,
+                  "comet_resize_bilinear_nhwc_into: c, ldy multiples of 8, ldy >= c, 16-B aligned");
+  COMET_CHECK_ARG(n * oh < (1ll << 31) && ow * (c / 8) < (1ll << 24) && ldy < (1ll << 24) && h < (1 << 30) && w < (1 << 30),
+                  "comet_resize_bilinear_nhwc_into: sizes out of range");
+  hipStream_t s = as_stream(stream);
+  const RowBlock rb = make_rowblock(n * oh, ow * (c / 8));
+  const unsigned gr = (unsigned)cdiv(rb.nrows, rb.RB);
+#define RSR(TI, TO) hipLaunchKernelGGL((resize_nhwc8_rows_kernel<TI, TO>), dim3(gr), dim3(256), 0, s, (const TI*)x, (TO*)y, rb, (int)c, (int)h, (int)w, (int)oh, (int)ow, add, (int)ldy)
+  if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RSR(float, float);
+  else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) RSR(float, __bf16);
+  else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) RSR(__bf16, __bf16);
+  else RSR(__bf16, float);
+#undef RSR
+  COMET_CHECK_LAUNCH("comet_resize_bilinear_nhwc_into");
   return COMET_OK;
 }

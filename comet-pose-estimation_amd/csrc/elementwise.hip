@@ -41,14 +41,38 @@ __device__ __forceinline__ float act_grad(int act, float p) {
   }
 }
 
+// d/dx of gelu_erf with the same branch-free erf (A&S 7.1.26, |err| <= 1.5e-7) and one exp shared
+// by the cdf and pdf terms (libm erff branches on |x| < 1 and made the GELU backward VALU-bound)
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __expf(-z * z);  // = exp(-x^2 / 2)
+  const float erf_v = copysignf(1.0f - p * t * e, x);
+  return 0.5f * (1.0f + erf_v) + x * (0.39894228040143267794f * e);
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_grad_t(float p) {
+  if constexpr (ACT == COMET_ACT_GELU) return gelu_grad_fast(p);
+  else if constexpr (ACT == COMET_ACT_RELU) return p > 0.f ? 1.f : 0.f;
+  else if constexpr (ACT == COMET_ACT_SIGMOID) { const float s = 1.f / (1.f + __expf(-p)); return s * (1.f - s); }
+  else return 1.f;
+}
+
 // Linear-layer backward prologue in one pass over dY [rows, cols] (cols % 8 == 0):
 // g = dY * act'(pre) (or dY), optionally stored (out, any dtype), and dbias[c] += sum_r g.
 // Block = 32 column groups of 8 x 8 row lanes; partial column sums meet in LDS, one atomic per
-// column per block.
-template <typename TP, typename TD, typename TO>
+// column per block. The activation and the presence of `out` are template parameters so the
+// row loop is branch-free: four rows per trip with all their loads issued first.
+template <typename TP, typename TD, typename TO, int ACT, bool HO>
 __global__ void __launch_bounds__(256)
-act_bwd_colsum_kernel(int act, const TP* __restrict__ pre, const TD* __restrict__ dy, TO* __restrict__ out,
+act_bwd_colsum_kernel(const TP* __restrict__ pre, const TD* __restrict__ dy, TO* __restrict__ out,
                       float* __restrict__ dbias, int64_t rows, int cols, int64_t chunk) {
+  constexpr bool HP = ACT != COMET_ACT_NONE;
   __shared__ float red[8][256];
   const int t = threadIdx.x, cl = t & 31, rl = t >> 5;
   const int c0 = blockIdx.x * 256 + cl * 8;
@@ -57,24 +81,37 @@ act_bwd_colsum_kernel(int act, const TP* __restrict__ pre, const TD* __restrict_
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  auto row_step = [&](int64_t r, float (&g)[8], const float (&x)[8]) {
+    if constexpr (HP) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] *= act_grad_t<ACT>(x[e]);
+    }
+    if constexpr (HO) {
+      // round first so the bias gradient sums exactly the values the GEMMs consume
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] = to_f32(from_f32<TO>(g[e]));
+      store8(out + r * cols + c0, g);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += g[e];
+  };
   if (c0 < cols) {
-    for (int64_t r = r0 + rl; r < r1; r += 8) {
-      float g[8];
+    int64_t r = r0 + rl;
+    for (; r + 24 < r1; r += 32) {
+      float g[4][8], x[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        load8(dy + (r + 8 * u) * cols + c0, g[u]);
+        if constexpr (HP) load8(pre + (r + 8 * u) * cols + c0, x[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) row_step(r + 8 * u, g[u], x[u]);
+    }
+    for (; r < r1; r += 8) {
+      float g[8], x[8];
       load8(dy + r * cols + c0, g);
-      if (pre) {
-        float x[8];
-        load8(pre + r * cols + c0, x);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) g[e] *= act_grad(act, x[e]);
-      }
-      if (out) {
-        // round first so the bias gradient sums exactly the values the GEMMs consume
-#pragma unroll
-        for (int e = 0; e < 8; ++e) g[e] = to_f32(from_f32<TO>(g[e]));
-        store8(out + r * cols + c0, g);
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += g[e];
+      if constexpr (HP) load8(pre + r * cols + c0, x);
+      row_step(r, g, x);
     }
   }
   if (!dbias) return;
@@ -243,13 +280,26 @@ extern "C" int comet_act_bwd_colsum(int act, int dtype_pre, const void* pre, int
   COMET_CHECK_ARG(rblocks <= 65535, "comet_act_bwd_colsum: too many rows");
   dim3 grid((unsigned)cblocks, (unsigned)rblocks);
   const void* P = act == COMET_ACT_NONE ? nullptr : pre;
-#define ABC(TP, TD, TO) \
-  hipLaunchKernelGGL((act_bwd_colsum_kernel<TP, TD, TO>), grid, dim3(256), 0, s, act, (const TP*)P, (const TD*)dy, (TO*)out, dbias, rows, (int)cols, chunk)
-#define ABC_O(TP, TD) do { if (dtype_out == COMET_F32) ABC(TP, TD, float); else ABC(TP, TD, __bf16); } while (0)
+  const bool ho = out != nullptr;
+#define ABC(TP, TD, TO, A, H) \
+  hipLaunchKernelGGL((act_bwd_colsum_kernel<TP, TD, TO, A, H>), grid, dim3(256), 0, s, (const TP*)P, (const TD*)dy, (TO*)out, dbias, rows, (int)cols, chunk)
+#define ABC_H(TP, TD, TO, A) do { if (ho) ABC(TP, TD, TO, A, true); else ABC(TP, TD, TO, A, false); } while (0)
+#define ABC_A(TP, TD, TO)                                                                   \
+  do {                                                                                      \
+    switch (act) {                                                                          \
+      case COMET_ACT_GELU: ABC_H(TP, TD, TO, COMET_ACT_GELU); break;                        \
+      case COMET_ACT_RELU: ABC_H(TP, TD, TO, COMET_ACT_RELU); break;                        \
+      case COMET_ACT_SIGMOID: ABC_H(TP, TD, TO, COMET_ACT_SIGMOID); break;                  \
+      default: ABC_H(TP, TD, TO, COMET_ACT_NONE); break;                                    \
+    }                                                                                       \
+  } while (0)
+#define ABC_O(TP, TD) do { if (dtype_out == COMET_F32) ABC_A(TP, TD, float); else ABC_A(TP, TD, __bf16); } while (0)
 #define ABC_D(TP) do { if (dtype_dy == COMET_F32) ABC_O(TP, float); else ABC_O(TP, __bf16); } while (0)
   if (dtype_pre == COMET_F32) ABC_D(float); else ABC_D(__bf16);
 #undef ABC_D
 #undef ABC_O
+#undef ABC_A
+#undef ABC_H
 #undef ABC
   COMET_CHECK_LAUNCH("comet_act_bwd_colsum");
   return COMET_OK;

@@ -7,6 +7,8 @@
 //
 // One wave per row; the row (<= 1024 columns) is held in registers, mean and variance are
 // two exact passes over the registers (wave shuffles), no LDS.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace comet {
@@ -184,6 +186,88 @@ ln_fwd_vec_kernel(const TX* __restrict__ x, const float* __restrict__ w, const f
   if (lane == 0) {
     if (mean_out) mean_out[row] = mean;
     if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
+// Persistent-row form of ln_fwd_vec_kernel: each wave walks rows wave_id, wave_id + waves, ... and
+// issues the next row's loads before reducing / storing the current one (a one-row-per-wave block
+// lives mostly in load latency, so the short blocks held the forward near 3.8 TB/s).
+template <typename TX, typename TY, int CH, int NK>
+__global__ void __launch_bounds__(256)
+ln_fwd_rows_kernel(const TX* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                   TY* __restrict__ y, __bf16* __restrict__ y2, float* __restrict__ mean_out,
+                   float* __restrict__ rstd_out, int64_t rows, int cols, int64_t ldx, int64_t ldy,
+                   int64_t ldy2, float eps, int relu) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float wv[NK][CH], bv[NK][CH];
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+#pragma unroll
+    for (int e = 0; e < CH; ++e) {
+      const int c = (lane + 64 * k) * CH + e;
+      wv[k][e] = (w && c < cols) ? w[c] : 1.f;
+      bv[k][e] = (b && c < cols) ? b[c] : 0.f;
+    }
+  float v[NK][CH], nx[NK][CH];
+  auto load_row = [&](int64_t r, float (&dst)[NK][CH]) {
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (lane + 64 * k) * CH;
+      if (c0 < cols) {
+        loadn<CH>(x + r * ldx + c0, dst[k]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < CH; ++e) dst[k][e] = 0.f;
+      }
+    }
+  };
+  load_row(row, v);
+  for (; row < rows; row += nw) {
+    const int64_t nrow = row + nw;
+    if (nrow < rows) load_row(nrow, nx);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+#pragma unroll
+      for (int e = 0; e < CH; ++e) s += v[k][e];
+    const float mean = wave_sum(s) / cols;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (lane + 64 * k) * CH;
+      if (c0 < cols)
+#pragma unroll
+        for (int e = 0; e < CH; ++e) { const float d = v[k][e] - mean; q += d * d; }
+    }
+    const float var = wave_sum(q) / cols;
+    const float rstd = rsqrtf(var + eps);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int c0 = (lane + 64 * k) * CH;
+      if (c0 >= cols) continue;
+      float o[CH];
+#pragma unroll
+      for (int e = 0; e < CH; ++e) {
+        float t = (v[k][e] - mean) * rstd;
+        if (w) t = t * wv[k][e];
+        if (b) t = t + bv[k][e];
+        if (relu) t = t > 0.f ? t : 0.f;
+        o[e] = t;
+      }
+      if (y) storen<CH>(y + row * ldy + c0, o);
+      if (y2) storen<CH>(y2 + row * ldy2 + c0, o);
+    }
+    if (lane == 0) {
+      if (mean_out) mean_out[row] = mean;
+      if (rstd_out) rstd_out[row] = rstd;
+    }
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+#pragma unroll
+      for (int e = 0; e < CH; ++e) v[k][e] = nx[k][e];
   }
 }
 
@@ -478,9 +562,21 @@ extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, cons
   const bool vec = cols % 8 == 0 && ldx % 8 == 0 && (y == nullptr || ldy % 8 == 0) && (y2 == nullptr || ldy2 % 8 == 0) &&
                    a32(x) && a32(y) && a32(y2);
   if (vec) {
-#define LNV(TX, TY, CH, NK)                                                                               \
-  hipLaunchKernelGGL((ln_fwd_vec_kernel<TX, TY, CH, NK>), grid, dim3(256), 0, s, (const TX*)x, weight, bias, \
-                     (TY*)y, (__bf16*)y2, mean, rstd, rows, (int)cols, ldx, ldy, ldy2, eps, relu)
+    // persistent rows: <= 8 workgroups (32 waves) per CU, each wave prefetching its next row
+    // (balanced: every wave gets the same number of rows +- 1); <= 2 rows per wave stays flat
+    const bool flat = rows <= 2 * 2048 * 4 || getenv("COMET_LN_FLAT") != nullptr;
+    const int64_t iters = cdiv(rows, 2048 * 4);
+    const dim3 grid_rows((unsigned)cdiv(cdiv(rows, iters), 4));
+#define LNV(TX, TY, CH, NK)                                                                                    \
+  do {                                                                                                         \
+    if (flat)                                                                                                  \
+      hipLaunchKernelGGL((ln_fwd_vec_kernel<TX, TY, CH, NK>), grid, dim3(256), 0, s, (const TX*)x, weight,      \
+                         bias, (TY*)y, (__bf16*)y2, mean, rstd, rows, (int)cols, ldx, ldy, ldy2, eps, relu);   \
+    else                                                                                                       \
+      hipLaunchKernelGGL((ln_fwd_rows_kernel<TX, TY, CH, NK>), grid_rows, dim3(256), 0, s, (const TX*)x,       \
+                         weight, bias, (TY*)y, (__bf16*)y2, mean, rstd, rows, (int)cols, ldx, ldy, ldy2, eps,  \
+                         relu);                                                                                \
+  } while (0)
 #define LNV_CH(TX, TY, CH)                                                                                 \
   do {                                                                                                     \
     const int nk = (int)cdiv(cols, 64 * CH);                                                               \

@@ -245,6 +245,12 @@ int comet_instnorm_nhwc(int dtype, const void* x, const void* res, void* y, int6
 int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, const void* x, void* y,
                           int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
                           int add, void* stream);
+/* NHWC resize into a channel slice of a wider NHWC tensor (output pixel pitch ldy elements):
+ * BasicEncoder's four up-sampled maps land directly in their torch.cat(dim=1) positions
+ * (blocks.py:97-107), so the 416-channel concat is never copied. c, ldy % 8 == 0. */
+int comet_resize_bilinear_nhwc_into(int dtype_in, int dtype_out, const void* x, void* y, int64_t n,
+                                    int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
+                                    int64_t ldy, int add, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Camera head (camera_predictor10.py:329-484) and encoders.

@@ -584,3 +584,123 @@ def test_attention_inner_batch_4d(D):
     xd = x.to(DEV)
     out = ops.attention(xd[..., :C], xd[..., C:2 * C], xd[..., 2 * C:], H)
     _close(out, ref, 2e-2, 2e-2, f"inner-batch attention D={D}")
+
+
+@pytest.mark.parametrize("cols,xdt,ydt", [(768, torch.float32, torch.bfloat16), (384, torch.float32, torch.float32),
+                                          (768, torch.bfloat16, torch.bfloat16), (1024, torch.float32, torch.bfloat16)])
+def test_layernorm_persistent_rows(cols, xdt, ydt, monkeypatch):
+    """Persistent-row LayerNorm forward (each wave walks several rows with the next row
+    prefetched): 20011 rows > 2048 x 4 waves, vs f64 and bit-exact vs the one-row-per-wave kernel."""
+    ops = _ops()
+    rows = 20011
+    x = (_rand(rows, cols, seed=120, scale=2.0) + 0.3).to(xdt)
+    w, b = _rand(cols, seed=121), _rand(cols, seed=122)
+    ref = F.layer_norm(x.double(), (cols,), w.double(), b.double(), 1e-5)
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    y, mean, rstd = ops.layernorm(xd, wd, bd, eps=1e-5, out_dtype=ydt, stats=True)
+    tol = 1e-5 if ydt == torch.float32 else 8e-3
+    _close(y, ref, tol, tol, f"ln rows {cols} {xdt}->{ydt}")
+    monkeypatch.setenv("COMET_LN_FLAT", "1")
+    y1, mean1, rstd1 = ops.layernorm(xd, wd, bd, eps=1e-5, out_dtype=ydt, stats=True)
+    assert torch.equal(mean, mean1) and torch.equal(rstd, rstd1)
+    tol1 = 1e-6 if ydt == torch.float32 else 8e-3  # one bf16 ulp if an fma contracts differently
+    _close(y, y1.double(), tol1, tol1, "ln rows vs one-row-per-wave")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_tracker_tokens_row_blocked(dtype, monkeypatch):
+    """comet_tracker_tokens (base_track_predictor.py:186-222 token assembly): row-blocked kernel
+    bit-identical to the flat element-wise kernel, incl. the zero pad columns."""
+    ops = _ops()
+    B, N, S, lat, corrdim = 2, 37, 5, 128, 324
+    tdim = 2 * (lat // 2) + 2 + corrdim + lat + 6
+    rows = B * N * S
+    coords = (_rand(rows, 2, seed=130) * 20).to(DEV)
+    feats = _rand(rows, lat, seed=131).to(DEV)
+    corr = _rand(rows, corrdim + 4, seed=132).to(DEV)[:, :corrdim]
+    pos = _rand(B * N, tdim, seed=133).to(DEV)
+    x1 = torch.empty(rows, tdim, device=DEV, dtype=dtype)
+    x2 = torch.empty(rows, tdim, device=DEV, dtype=dtype)
+    ops.tracker_tokens(coords, feats, lat, corr, corrdim, pos, tdim, x1, rows, S)
+    monkeypatch.setenv("COMET_TOKENS_FLAT", "1")
+    ops.tracker_tokens(coords, feats, lat, corr, corrdim, pos, tdim, x2, rows, S)
+    assert torch.equal(x1, x2)
+    # spot check against the definition: frame-0 rows have zero flow -> emb = sin(0)/cos(0)
+    E = lat // 2
+    r0 = x1[0].float().cpu() - pos[0].cpu()
+    tol = 1e-6 if dtype == torch.float32 else 5e-2
+    assert (r0[0:2 * E:2].abs() <= tol).all() and ((r0[1:2 * E:2] - 1).abs() <= tol).all()
+
+
+def _corr_ref(pyr, radius, feats, coords, B, N, S):
+    """CorrBlock.corr + CorrBlock.sample (blocks.py:351-429) in f64: per level, the correlation map
+    f . fmap / sqrt(C) sampled bilinearly (zeros padding, align_corners=True pixel coordinates) at
+    (x/2^l + i - r, y/2^l + j - r), window index i on x."""
+    C = pyr[0].shape[-1]
+    win = 2 * radius + 1
+    out = torch.zeros(B * N * S, len(pyr) * win * win, dtype=torch.float64)
+    d = torch.arange(-radius, radius + 1, dtype=torch.float64)
+    for l, fm in enumerate(pyr):
+        fm = fm.double().cpu()
+        H, W = fm.shape[1], fm.shape[2]
+        for t in range(B * N * S):
+            s = t % S
+            b = t // S // N
+            cmap = fm[b * S + s] @ feats[t].double().cpu() / math.sqrt(C)  # [H, W]
+            xl = coords[t, 0].item() / 2 ** l
+            yl = coords[t, 1].item() / 2 ** l
+            X = (xl + d).view(win, 1).expand(win, win)   # i on x
+            Y = (yl + d).view(1, win).expand(win, win)   # j on y
+            x0, y0 = torch.floor(X), torch.floor(Y)
+            v = torch.zeros(win, win, dtype=torch.float64)
+            for dx in (0, 1):
+                for dy in (0, 1):
+                    xi, yi = x0 + dx, y0 + dy
+                    wgt = (1 - (X - xi).abs()) * (1 - (Y - yi).abs())
+                    ok = (xi >= 0) & (xi < W) & (yi >= 0) & (yi < H)
+                    g = cmap[yi.clamp(0, H - 1).long(), xi.clamp(0, W - 1).long()]
+                    v += torch.where(ok, g * wgt, torch.zeros_like(g))
+            out[t, l * win * win:(l + 1) * win * win] = v.reshape(-1)
+    return out
+
+
+@pytest.mark.parametrize("C,radius,dtype", [(128, 4, torch.bfloat16), (128, 3, torch.float32), (32, 3, torch.bfloat16),
+                                            (128, 6, torch.bfloat16), (32, 6, torch.float32), (128, 1, torch.bfloat16)])
+def test_corr_sample_vs_f64(C, radius, dtype, monkeypatch):
+    """comet_corr_sample (fused CorrBlock corr + window sampling) vs an f64 restatement (tracks
+    near and beyond the map border); the opt-in hoisted-load variant equals the default kernel."""
+    ops = _ops()
+    B, N, S, levels = 2, 3, 2, 3
+    H0 = 20
+    pyr = [_rand(B * S, H0 >> l, H0 >> l, C, seed=140 + l).to(dtype).to(DEV) for l in range(levels)]
+    rows = B * N * S
+    feats = _rand(rows, C, seed=150)
+    coords = torch.rand(rows, 2, generator=torch.Generator().manual_seed(151)) * (H0 + 8) - 4
+    win = 2 * radius + 1
+    out = torch.full((rows, levels * win * win + 5), 7.0, device=DEV)
+    ops.corr_sample(pyr, radius, feats.to(DEV), coords.to(DEV), out, 2, B, N, S)
+    ref = _corr_ref(pyr, radius, feats, coords, B, N, S)
+    _close(out[:, 2:2 + levels * win * win], ref, 1e-4, 1e-4, f"corr C={C} r={radius}")
+    assert (out[:, :2] == 7.0).all() and (out[:, 2 + levels * win * win:] == 7.0).all()
+    monkeypatch.setenv("COMET_CORR_PF", "1")
+    out1 = torch.full_like(out, 7.0)
+    ops.corr_sample(pyr, radius, feats.to(DEV), coords.to(DEV), out1, 2, B, N, S)
+    _close(out1, out.double(), 1e-6, 1e-6, "hoisted-load corr vs default kernel")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_resize_into_channel_slices(dtype):
+    """BasicEncoder concat (blocks.py:102-107): four maps resized straight into their channel
+    slices of one NHWC tensor equal torch.cat of the separate resizes."""
+    ops = _ops()
+    n, oh, ow = 3, 24, 24
+    parts = [_rand(n, 48, 48, 64, seed=160), _rand(n, 24, 24, 96, seed=161), _rand(n, 12, 12, 128, seed=162),
+             _rand(n, 6, 6, 128, seed=163)]
+    parts = [p.to(dtype).to(DEV) for p in parts]
+    x = torch.full((n, oh, ow, 416), 3.0, device=DEV, dtype=dtype)
+    c0 = 0
+    for p in parts:
+        ops.resize_bilinear_into(p, x[..., c0:c0 + p.shape[-1]])
+        c0 += p.shape[-1]
+    ref = torch.cat([ops.resize_bilinear(p, oh, ow, nhwc=True) for p in parts], dim=-1)
+    assert torch.equal(x, ref)
