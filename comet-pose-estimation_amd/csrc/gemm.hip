@@ -1396,10 +1396,13 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
 int big_bn(const comet_gemm_args& a) {
   if (getenv("COMET_GEMM_NO_BIG") != nullptr) return 0;
   if (a.dtype_ab != COMET_BF16 || a.convert_a || a.convert_b) return 0;
-  if (a.batch[0] * a.batch[1] != 1 || a.k % 64 != 0 || a.k == 0) return 0;
+  const bool wide = a.layout_a == 1 || a.layout_b == 1;  // transposed: dX / dW shapes
+  // K % 64 != 0: dW shapes over a ragged token count (e.g. 8 x 15 x 577) run the 64-multiple part
+  // here as split-K partials and the < 64 remainder as one more partial (comet_gemm)
+  const bool ragged_ok = wide && a.k >= 1024 && getenv("COMET_GEMM_NO_RAGGED") == nullptr;
+  if (a.batch[0] * a.batch[1] != 1 || (a.k % 64 != 0 && !ragged_ok) || a.k == 0) return 0;
   if ((uintptr_t)a.a % 16 != 0 || (uintptr_t)a.b % 16 != 0 || a.lda % 8 != 0 || a.ldb % 8 != 0) return 0;
   if ((a.layout_a == 1 && a.m % 8 != 0) || (a.layout_b == 1 && a.n % 8 != 0)) return 0;
-  const bool wide = a.layout_a == 1 || a.layout_b == 1;  // transposed: dX / dW shapes
   if (!wide && a.m < 4096) return 0;
   if (a.m < 256 || a.n < 128) return 0;
   const int64_t w256 = cdiv(a.n, 256) * 256 - a.n, w128 = cdiv(a.n, 128) * 128 - a.n;
@@ -1413,16 +1416,20 @@ struct Plan {
   int bn;        // kind 1, 3: column tile
   int splits;    // requested K splits (before the workspace check)
   int bm = 0;    // kind 3: row tile
+  int tail = 0;  // kind 1: K % 64 (one extra split-K partial computed by the 128 x 128 kernel)
 };
 
 Plan make_plan(const comet_gemm_args& a);
 int64_t plan_workspace(const comet_gemm_args& a, const Plan& p) {
+  if (p.tail) return (int64_t)(p.splits + 1) * a.m * a.n * (int64_t)sizeof(float);
   if (p.splits <= 1) return 0;
   return (int64_t)p.splits * a.batch[0] * a.batch[1] * a.m * a.n * (int64_t)sizeof(float);
 }
 
+// extra > 0: split mode even for one split, and the reduce also sums `extra` partial slots that
+// precede a.workspace (the ragged-K remainder)
 template <typename TC, int BN, int LA, int LB>
-int launch_big(const comet_gemm_args& a, int splits, hipStream_t s) {
+int launch_big(const comet_gemm_args& a, int splits, hipStream_t s, int extra = 0) {
   auto v8 = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 32 == 0 && ld % 8 == 0); };
   const int vec = a.n % 8 == 0 && v8(a.c, a.ldc) && v8(a.resid, a.ldr) && v8(a.aux, a.ldaux);
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, vec};
@@ -1435,7 +1442,7 @@ int launch_big(const comet_gemm_args& a, int splits, hipStream_t s) {
   }
   Split sp{reinterpret_cast<float*>(a.workspace), kchunk};
   dim3 grid((unsigned)(tiles_m * tiles_n), (unsigned)splits);
-  if (splits > 1) {
+  if (splits > 1 || extra > 0) {
     hipLaunchKernelGGL((big::gemm_big_kernel<float, BN, LA, LB, true>), grid, dim3(big::NT), 0, s,
                        (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (float*)nullptr, a.ldc, a.m, a.n, a.k,
                        (int)tiles_n, e, sp);
@@ -1443,7 +1450,8 @@ int launch_big(const comet_gemm_args& a, int splits, hipStream_t s) {
     const int64_t work = a.m * cdiv(a.n, 4);
     int64_t blocks = cdiv(work, 256);
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL((splitk_reduce_kernel<TC>), dim3((unsigned)blocks), dim3(256), 0, s, sp.ws, splits, (int64_t)1,
+    hipLaunchKernelGGL((splitk_reduce_kernel<TC>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       sp.ws - (int64_t)extra * a.m * a.n, splits + extra, (int64_t)1,
                        (int64_t)1, (TC*)a.c, a.ldc, (int64_t)0, (int64_t)0, a.m, a.n, e);
     COMET_CHECK_LAUNCH("comet_gemm split-K reduce");
     return COMET_OK;
@@ -1456,11 +1464,11 @@ int launch_big(const comet_gemm_args& a, int splits, hipStream_t s) {
 }
 
 template <typename TC, int BN>
-int launch_big_layout(const comet_gemm_args& a, int splits, hipStream_t s) {
-  if (a.layout_a == 0 && a.layout_b == 0) return launch_big<TC, BN, 0, 0>(a, splits, s);
-  if (a.layout_a == 0 && a.layout_b == 1) return launch_big<TC, BN, 0, 1>(a, splits, s);
-  if (a.layout_a == 1 && a.layout_b == 0) return launch_big<TC, BN, 1, 0>(a, splits, s);
-  return launch_big<TC, BN, 1, 1>(a, splits, s);
+int launch_big_layout(const comet_gemm_args& a, int splits, hipStream_t s, int extra = 0) {
+  if (a.layout_a == 0 && a.layout_b == 0) return launch_big<TC, BN, 0, 0>(a, splits, s, extra);
+  if (a.layout_a == 0 && a.layout_b == 1) return launch_big<TC, BN, 0, 1>(a, splits, s, extra);
+  if (a.layout_a == 1 && a.layout_b == 0) return launch_big<TC, BN, 1, 0>(a, splits, s, extra);
+  return launch_big<TC, BN, 1, 1>(a, splits, s, extra);
 }
 
 // ---- host side --------------------------------------------------------------------------
@@ -1501,7 +1509,7 @@ Plan make_plan(const comet_gemm_args& a) {
         sp = s2 < 1 ? 1 : (int)s2;
       }
     }
-    return Plan{1, bn, sp};
+    return Plan{1, bn, sp, 0, (int)(a.k % 64)};
   }
   return Plan{2, 0, choose_splits(a)};
 }
@@ -1878,7 +1886,35 @@ extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   const Plan plan = make_plan(a);
   if (plan.kind == 0) return a.dtype_c == COMET_BF16 ? launch_skinny<__bf16>(a, s) : launch_skinny<float>(a, s);
   if (plan.kind == 3) return a.dtype_c == COMET_BF16 ? launch_pp<__bf16>(a, s) : launch_pp<float>(a, s);
-  if (plan.kind == 1) {
+  if (plan.kind == 1 && plan.tail && a.workspace != nullptr && a.workspace_bytes >= plan_workspace(a, plan)) {
+    // slot 0: the K % 64 remainder (128 x 128 kernel, plain f32 output); slots 1..: the 256-row
+    // kernel's split partials over the 64-multiple part; one reduce applies the epilogue
+    const int64_t kt = plan.tail, km = a.k - kt;
+    float* ws = reinterpret_cast<float*>(a.workspace);
+    comet_gemm_args t{};
+    t.dtype_ab = a.dtype_ab;
+    t.dtype_c = COMET_F32;
+    t.layout_a = a.layout_a;
+    t.layout_b = a.layout_b;
+    t.m = a.m; t.n = a.n; t.k = kt;
+    t.a = reinterpret_cast<const __bf16*>(a.a) + (a.layout_a == 0 ? km : km * a.lda);
+    t.b = reinterpret_cast<const __bf16*>(a.b) + (a.layout_b == 0 ? km : km * a.ldb);
+    t.lda = a.lda; t.ldb = a.ldb;
+    t.c = ws; t.ldc = a.n;
+    t.batch[0] = t.batch[1] = 1;
+    t.alpha = 1.f;
+    t.split_k = 1;
+    int rc = dispatch_layout<__bf16, float>(t, s);
+    if (rc != COMET_OK) return rc;
+    comet_gemm_args m = a;
+    m.k = km;
+    m.workspace = ws + a.m * a.n;
+    m.workspace_bytes = a.workspace_bytes - a.m * a.n * (int64_t)sizeof(float);
+    if (plan.bn == 256)
+      return a.dtype_c == COMET_BF16 ? launch_big_layout<__bf16, 256>(m, plan.splits, s, 1) : launch_big_layout<float, 256>(m, plan.splits, s, 1);
+    return a.dtype_c == COMET_BF16 ? launch_big_layout<__bf16, 128>(m, plan.splits, s, 1) : launch_big_layout<float, 128>(m, plan.splits, s, 1);
+  }
+  if (plan.kind == 1 && !plan.tail) {
     int sp = plan.splits;
     if (sp > 1 && (a.workspace == nullptr || a.workspace_bytes < plan_workspace(a, plan))) sp = 1;
     if (plan.bn == 256)

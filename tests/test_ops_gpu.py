@@ -704,3 +704,31 @@ def test_resize_into_channel_slices(dtype):
         c0 += p.shape[-1]
     ref = torch.cat([ops.resize_bilinear(p, oh, ow, nhwc=True) for p in parts], dim=-1)
     assert torch.equal(x, ref)
+
+
+@pytest.mark.parametrize("la,lb", [(1, 1), (0, 1), (1, 0)])
+@pytest.mark.parametrize("mnk", [(256, 512, 5000), (512, 768, 1100), (768, 256, 4161)])
+@pytest.mark.parametrize("out", [torch.float32, torch.bfloat16])
+def test_gemm_256_tile_ragged_k(la, lb, mnk, out, monkeypatch):
+    """dW-shaped GEMMs with K % 64 != 0 (token counts like 8 x 15 x 577): the 64-multiple part as
+    256-row split-K partials plus the remainder as one more partial, one reduce with the bias
+    epilogue; vs f64 and vs the generic 128 x 128 path."""
+    ops = _ops()
+    M, N, K = mnk
+    A = _rand(M, K, seed=170).to(torch.bfloat16)
+    B = _rand(N, K, seed=171).to(torch.bfloat16)
+    bias = _rand(N, seed=172)
+    ref = A.double() @ B.double().t() + bias.double()
+    Ad = (A if la == 0 else A.t().contiguous()).to(DEV)
+    Bd = (B if lb == 0 else B.t().contiguous()).to(DEV)
+    res = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("COMET_GEMM_NO_RAGGED", env)
+        C = torch.empty(M, N, device=DEV, dtype=out)
+        ops.gemm_raw(Ad, Bd, C, m=M, n=N, k=K, layout_a=la, lda=(K if la == 0 else M), layout_b=lb,
+                     ldb=(K if lb == 0 else N), ldc=N, bias=bias.to(DEV), bias_mode=1)
+        res.append(C)
+    tol = 1e-3 if out == torch.float32 else 8e-3
+    _close(res[0], ref, tol, 1e-3 * math.sqrt(K), f"ragged-K la={la} lb={lb} {mnk}")
+    _close(res[0], res[1].double(), tol, 1e-3 * math.sqrt(K), "ragged-K vs generic path")
