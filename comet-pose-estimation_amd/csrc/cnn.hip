@@ -142,6 +142,46 @@ resize_nhwc8_rows_kernel(const TI* __restrict__ x, TO* __restrict__ y, RowBlock 
   }
 }
 
+// Small images (the fine ShallowEncoder's 16 x 16 -> 31 x 31 patch maps, 65536 of them): one
+// workgroup per image stages the whole input image in LDS (<= 32 KiB) and writes the output
+// image as one contiguous run of 16-B stores; the row kernel re-read each input pixel from L2 for
+// every output it touches (4 x 16 B of L2 reads per 16 B written).
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+resize_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, int c, int h, int w, int oh, int ow,
+                        int add) {
+  extern __shared__ uint4 img_lds[];
+  const TI* img = reinterpret_cast<const TI*>(img_lds);
+  const int64_t ni = blockIdx.x;
+  const int nvec = (int)((int64_t)h * w * c * (int)sizeof(TI) / 16);
+  const uint4* src = reinterpret_cast<const uint4*>(x + ni * h * w * c);
+  for (int i = threadIdx.x; i < nvec; i += 256) img_lds[i] = src[i];
+  __syncthreads();
+  const int cg8 = c / 8, items = oh * ow * cg8;
+  TO* yo = y + ni * oh * ow * c;
+  for (int it = threadIdx.x; it < items; it += 256) {
+    const int pix = it / cg8, cg = it - pix * cg8;
+    const int oy = pix / ow, ox = pix - oy * ow;
+    int64_t y0, y1, x0, x1;
+    float fy, fx;
+    ac_coord(oy, h, oh, y0, y1, fy);
+    ac_coord(ox, w, ow, x0, x1, fx);
+    float v00[8], v01[8], v10[8], v11[8];
+    load8(img + ((int)y0 * w + (int)x0) * c + cg * 8, v00);
+    load8(img + ((int)y0 * w + (int)x1) * c + cg * 8, v01);
+    load8(img + ((int)y1 * w + (int)x0) * c + cg * 8, v10);
+    load8(img + ((int)y1 * w + (int)x1) * c + cg * 8, v11);
+    float o[8];
+    if (add) load8(yo + (int64_t)it * 8, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = (1.f - fy) * ((1.f - fx) * v00[e] + fx * v01[e]) + fy * ((1.f - fx) * v10[e] + fx * v11[e]);
+      o[e] = add ? o[e] + v : v;
+    }
+    store8(yo + (int64_t)it * 8, o);
+  }
+}
+
 inline unsigned g1d(int64_t n) {
   int64_t g = cdiv(n, 256);
   return (unsigned)(g > 16384 ? 16384 : (g < 1 ? 1 : g));
@@ -174,6 +214,19 @@ extern "C" int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, cons
                                      int64_t ow, int add, void* stream) {
   COMET_CHECK_ARG(x && y && n > 0 && c > 0 && h > 0 && w > 0 && oh > 0 && ow > 0, "comet_resize_bilinear: bad args");
   hipStream_t s = as_stream(stream);
+  const int esz = dtype_in == COMET_F32 ? 4 : 2;
+  if (nhwc && c % 8 == 0 && ((uintptr_t)x | (uintptr_t)y) % 16 == 0 && h * w * c * esz <= 32768 &&
+      oh * ow * c < (1ll << 30) && n < (1ll << 31) && getenv("COMET_RESIZE_ROWS") == nullptr) {
+    const size_t lds = (size_t)(h * w * c * esz);
+#define RSI(TI, TO) hipLaunchKernelGGL((resize_nhwc8_img_kernel<TI, TO>), dim3((unsigned)n), dim3(256), lds, s, (const TI*)x, (TO*)y, (int)c, (int)h, (int)w, (int)oh, (int)ow, add)
+    if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RSI(float, float);
+    else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) RSI(float, __bf16);
+    else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) RSI(__bf16, __bf16);
+    else RSI(__bf16, float);
+#undef RSI
+    COMET_CHECK_LAUNCH("comet_resize_bilinear");
+    return COMET_OK;
+  }
   if (nhwc && c % 8 == 0 && ((uintptr_t)x | (uintptr_t)y) % 32 == 0 && n * oh < (1ll << 31) &&
       ow * (c / 8) < (1ll << 24) && h < (1 << 30) && w < (1 << 30) && getenv("COMET_RESIZE_FLAT") == nullptr) {
     const RowBlock rb = make_rowblock(n * oh, ow * (c / 8));
