@@ -67,7 +67,9 @@ attn_fwd_kernel(const T* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 15, hg = lane >> 4;
-  const int64_t bh = blockIdx.y;
+  int bx, by;
+  xcd_remap2(bx, by);
+  const int64_t bh = by;
   const int64_t b = bh / heads, h = bh % heads;
   const int64_t bo = b / in.n, bi = b % in.n;
   Q += bo * sq_b + bi * in.sq + h * sq_h;
@@ -79,7 +81,7 @@ attn_fwd_kernel(const T* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_
   for (int i = tid; i < 64 * KP; i += 256) { Ks[i] = T(0.f); Vs[i] = T(0.f); }
 
   // ---- Q fragments (registers) ----
-  const int q = blockIdx.x * 64 + wid * 16 + li;
+  const int q = bx * 64 + wid * 16 + li;
   const bool qok = q < lq;
   constexpr int NQC = BF ? DA / 32 : DA / 16;
   typedef typename std::conditional<BF, bf16x8, f32x4>::type qfrag_t;
@@ -265,7 +267,9 @@ attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, i
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 15, hg = lane >> 4;
-  const int64_t bh = blockIdx.y;
+  int bx, by;
+  xcd_remap2(bx, by);
+  const int64_t bh = by;
   const int64_t b = bh / heads, h = bh % heads;
   const int64_t bo = b / in.n, bi = b % in.n;
   Q += bo * sq_b + bi * in.sq + h * sq_h;
@@ -281,7 +285,7 @@ attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, i
   int qrow[QG];
 #pragma unroll
   for (int g = 0; g < QG; ++g) {
-    qrow[g] = blockIdx.x * (64 * QG) + (wid * QG + g) * 16 + li;
+    qrow[g] = bx * (64 * QG) + (wid * QG + g) * 16 + li;
 #pragma unroll
     for (int c = 0; c < NQC; ++c) {
       const int d0 = 32 * c + 8 * hg;

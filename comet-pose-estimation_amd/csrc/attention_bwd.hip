@@ -97,7 +97,9 @@ attn_bwd_dkdv2_kernel(BwdPtrs p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 15, g = lane >> 4, qq = li >> 2, pp = li & 3;
-  const int64_t bh = blockIdx.y, b = bh / p.heads, h = bh % p.heads;
+  int bx, by;
+  xcd_remap2(bx, by);
+  const int64_t bh = by, b = bh / p.heads, h = bh % p.heads;
   const __bf16* Q = p.q + b * p.sq_b + h * p.sq_h;
   const __bf16* K = p.k + b * p.sk_b + h * p.sk_h;
   const __bf16* V = p.v + b * p.sv_b + h * p.sv_h;
@@ -115,7 +117,7 @@ attn_bwd_dkdv2_kernel(BwdPtrs p) {
   f32x4 dv[G][DT], dk[G][DT];
 #pragma unroll
   for (int k = 0; k < G; ++k) {
-    key0[k] = blockIdx.x * (64 * G) + (wid * G + k) * 16;
+    key0[k] = bx * (64 * G) + (wid * G + k) * 16;
     load_frags<D>(K, p.sk_l, key0[k] + li, key0[k] + li < p.lk, g, kf[k]);
     load_frags<D>(V, p.sv_l, key0[k] + li, key0[k] + li < p.lk, g, vf[k]);
 #pragma unroll
@@ -233,7 +235,9 @@ attn_bwd_dq2_kernel(BwdPtrs p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int li = lane & 15, g = lane >> 4, qq = li >> 2, pp = li & 3;
-  const int64_t bh = blockIdx.y, b = bh / p.heads, h = bh % p.heads;
+  int bx, by;
+  xcd_remap2(bx, by);
+  const int64_t bh = by, b = bh / p.heads, h = bh % p.heads;
   const __bf16* Q = p.q + b * p.sq_b + h * p.sq_h;
   const __bf16* K = p.k + b * p.sk_b + h * p.sk_h;
   const __bf16* V = p.v + b * p.sv_b + h * p.sv_h;
@@ -250,7 +254,7 @@ attn_bwd_dq2_kernel(BwdPtrs p) {
   f32x4 acc[G][DT];
 #pragma unroll
   for (int k = 0; k < G; ++k) {
-    qrow[k] = blockIdx.x * (64 * G) + (wid * G + k) * 16 + li;
+    qrow[k] = bx * (64 * G) + (wid * G + k) * 16 + li;
     const bool ok = qrow[k] < p.lq;
     load_frags<D>(Q, p.sq_l, qrow[k], ok, g, qf[k]);
     load_frags<D>(Gd, p.sd_l, qrow[k], ok, g, gf[k]);

@@ -153,6 +153,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + local;
 }
 
+// (x, y) block coordinates of a 2-D grid remapped so that consecutive x of one y run on one XCD:
+// the hardware deals linear ids (x fastest) round-robin over the 8 XCDs, so without this the
+// query / key tiles of one attention head (x) are spread over every XCD and each XCD's L2 fetches
+// that head's shared operand again.
+__device__ __forceinline__ void xcd_remap2(int& x, int& y) {
+  const int gx = gridDim.x;
+  const int r = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gridDim.y);
+  y = r / gx;
+  x = r - y * gx;
+}
+
 // Row-blocked NHWC launches (resize / pooling): R = items per output row (ow x channel groups),
 // a 256-thread block covers RB = max(1, 256 / R) output rows (n, oy) and loops over a row's items
 // when R > 256. Index math is 32-bit and done once per thread, not per element (the flat 64-bit
