@@ -158,16 +158,27 @@ struct MultiPtr {
   int count;
 };
 
+// Few workgroups (SQ_NORM_BLOCKS) and 16-B loads: the sum ends in one atomic per workgroup on a
+// single address, and 8192 of them serialised at L2 cost ~90 us per launch.
+constexpr int SQ_NORM_BLOCKS = 1024;
 __global__ void sq_norm_kernel(MultiPtr mp, float* __restrict__ out) {
   __shared__ float scratch[4];
   float s = 0.f;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int t = 0; t < mp.count; ++t) {
     const float* x = mp.g[t];
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < mp.n[t]; i += stride) {
-      const float v = x[i];
-      s += v * v;
+    const int64_t n = mp.n[t];
+    int64_t head = ((16 - ((uintptr_t)x & 15)) & 15) / 4;  // scalars before the first 16-B boundary
+    if (head > n) head = n;
+    const int64_t nv = (n - head) / 4;
+    const float4* xv = reinterpret_cast<const float4*>(x + head);
+    for (int64_t i = tid; i < nv; i += stride) {
+      const float4 v = xv[i];
+      s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
     }
+    for (int64_t i = tid; i < head; i += stride) s += x[i] * x[i];
+    for (int64_t i = head + nv * 4 + tid; i < n; i += stride) s += x[i] * x[i];
   }
   s = block_sum<4>(s, scratch);
   if (threadIdx.x == 0) atomicAdd(out, s);
@@ -337,7 +348,9 @@ extern "C" int comet_sq_norm_multi(const float* const* ptrs, const int64_t* size
       mp.n[i] = sizes[base + i];
       total += mp.n[i];
     }
-    hipLaunchKernelGGL(sq_norm_kernel, dim3(grid_for(total / 4 + 1)), dim3(256), 0, s, mp, out);
+    int64_t g = cdiv(total / 4 + 1, 256);
+    if (g > SQ_NORM_BLOCKS) g = SQ_NORM_BLOCKS;
+    hipLaunchKernelGGL(sq_norm_kernel, dim3((unsigned)g), dim3(256), 0, s, mp, out);
     COMET_CHECK_LAUNCH("comet_sq_norm_multi");
   }
   return COMET_OK;

@@ -760,3 +760,20 @@ def test_resize_nhwc_whole_image(dtype, n, c, h, w, oh, ow, add, monkeypatch):
     _close(outs[0].permute(0, 3, 1, 2), ref, tol, tol, f"resize img {dtype} {(n, c, h, w, oh, ow, add)}")
     tol1 = 1e-5 if dtype == torch.float32 else 8e-3  # fma contraction may differ between the kernels
     _close(outs[0], outs[1].double(), tol1, tol1, "whole-image vs row kernel")
+
+
+def test_sq_norm_multi_vectorised_and_ragged():
+    """comet_sq_norm_multi (clip_grad_norm_'s total norm, train_util.py:311-332): 16-B loads with
+    scalar heads / tails for unaligned views and ragged sizes, > 24 tensors (several launches)."""
+    import ctypes
+    from comet_amd import _lib as L
+    from comet_amd import ops
+    base = _rand(3_000_000, seed=190).to(DEV)
+    views = [base[1:1 + 1_000_003], base[8:8 + 17], base[1_100_001:1_100_001 + 5], base[2_000_000:2_900_000]]
+    views += [base[100 + 37 * i: 100 + 37 * i + 3 + i] for i in range(30)]
+    out = torch.zeros(1, device=DEV)
+    arr = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
+    sz = (ctypes.c_int64 * len(views))(*[v.numel() for v in views])
+    L.check(L.load().comet_sq_norm_multi(arr, sz, len(views), out.data_ptr(), ops.stream()), "sq_norm")
+    ref = sum((v.double().cpu() ** 2).sum() for v in views)
+    _close(out, ref.reshape(1), 1e-5, 0, "sq_norm_multi")
