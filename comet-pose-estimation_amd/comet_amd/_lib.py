@@ -95,6 +95,7 @@ SIGNATURES = {
     "comet_attn_delta": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "comet_attn_dsoftmax": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, _F, c_vp]),
     "comet_cast": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_vp]),
+    "comet_cast_multi_f32_bf16": (_INT, [c_vp, c_vp, c_vp, _INT, c_vp]),
     "comet_act_bwd": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_vp, _INT, c_i64, c_vp]),
     "comet_axpby": (_INT, [c_vp, c_vp, _F, _F, c_i64, c_vp]),
     "comet_act_bwd_colsum": (_INT, [_INT, _INT, c_vp, _INT, c_vp, _INT, c_vp, c_vp, c_i64, c_i64, _INT, c_vp]),

@@ -57,13 +57,42 @@ def wcast(p, dt=None):
         return hit
     c = ops.cast(p.detach(), dt)
     _wcache[key] = c
+    _wsrc[key] = p.detach()
     return c
+
+
+_wsrc = {}
+
+
+def refresh_weight_cache(params):
+    """Re-cast, in place and in one multi-tensor launch, the cached bf16 copies of `params` (and
+    of contiguous views of them) after an optimizer step updated them; other cached entries of
+    those params are dropped (re-cast at next use)."""
+    spans = [(p.data_ptr(), p.data_ptr() + p.numel() * p.element_size()) for p in params]
+
+    def ptr(k):
+        return k[1] if k[0] == "conv" else k[0]
+    hits = [k for k in _wcache if any(lo <= ptr(k) < hi for lo, hi in spans)]
+    src, dst = [], []
+    for k in hits:
+        s = _wsrc.get(k)
+        d = _wcache[k]
+        if (s is not None and s.dtype == torch.float32 and d.dtype == torch.bfloat16 and s.is_contiguous()
+                and d.is_contiguous() and s.numel() == d.numel()):
+            src.append(s)
+            dst.append(d)
+        else:
+            del _wcache[k]
+            _wsrc.pop(k, None)
+    if src:
+        ops.cast_multi_f32_bf16(src, dst)
 
 
 def invalidate_weight_cache(params=None):
     """Drop cached copies of `params` (all when None); called after every optimizer step."""
     if params is None:
         _wcache.clear()
+        _wsrc.clear()
         return
     spans = [(p.data_ptr(), p.data_ptr() + p.numel() * p.element_size()) for p in params]
 
@@ -71,6 +100,7 @@ def invalidate_weight_cache(params=None):
         return k[1] if k[0] == "conv" else k[0]
     for k in [k for k in _wcache if any(lo <= ptr(k) < hi for lo, hi in spans)]:
         del _wcache[k]
+        _wsrc.pop(k, None)
 
 
 def _needs_grad(*ts):

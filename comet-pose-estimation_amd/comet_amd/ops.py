@@ -425,6 +425,15 @@ def resize_bilinear(x, oh, ow, nhwc, out=None, add=False, out_dtype=None):
     return out
 
 
+def cast_multi_f32_bf16(srcs, dsts):
+    """dst[i].copy_(src[i]) f32 -> bf16 (contiguous, equal numel) in few launches."""
+    n = len(srcs)
+    S = (ctypes.c_void_p * n)(*[t.data_ptr() for t in srcs])
+    D = (ctypes.c_void_p * n)(*[t.data_ptr() for t in dsts])
+    Z = (ctypes.c_int64 * n)(*[t.numel() for t in srcs])
+    L.check(L.load().comet_cast_multi_f32_bf16(S, D, Z, n, stream()), "cast_multi")
+
+
 def resize_bilinear_into(x, out, add=False):
     """NHWC x [n, h, w, c] resized into out [n, oh, ow, c], a channel slice of a wider NHWC tensor
     (out.stride() == (oh*ow*ld, ow*ld, ld, 1))."""

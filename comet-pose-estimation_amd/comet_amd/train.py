@@ -104,7 +104,7 @@ class CometAdamW:
                                            float(self.eps), float(self.weight_decay), self.step_count,
                                            None if sq is None else sq.data_ptr(), float(max_norm or 0.0), ops.stream()),
                 "adamw")
-        F.invalidate_weight_cache(ps)
+        F.refresh_weight_cache(ps)
         self.last_sqnorm = sq
         return sq
 

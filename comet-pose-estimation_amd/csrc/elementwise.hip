@@ -212,6 +212,36 @@ __global__ void adamw_kernel(MultiPtr mp, float lr, float b1, float b2, float ep
   }
 }
 
+// f32 -> bf16 for many tensors in one launch (the bf16 copies of the trainable weights, refreshed
+// after every optimizer step instead of ~125 per-tensor casts at first use in the next forward)
+constexpr int CAST_MAX = 48;
+struct CastPtrs {
+  const float* s[CAST_MAX];
+  __bf16* d[CAST_MAX];
+  int64_t n[CAST_MAX];
+  int count;
+};
+
+__global__ void __launch_bounds__(256) cast_multi_kernel(CastPtrs cp) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int t = 0; t < cp.count; ++t) {
+    const float* x = cp.s[t];
+    __bf16* y = cp.d[t];
+    const int64_t n = cp.n[t];
+    if ((((uintptr_t)x & 15) | ((uintptr_t)y & 7)) == 0) {
+      const int64_t nv = n / 4;
+      for (int64_t i = tid; i < nv; i += stride) {
+        const float4 v = reinterpret_cast<const float4*>(x)[i];
+        reinterpret_cast<uint2*>(y)[i] = uint2{pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w)};
+      }
+      for (int64_t i = nv * 4 + tid; i < n; i += stride) y[i] = static_cast<__bf16>(x[i]);
+    } else {
+      for (int64_t i = tid; i < n; i += stride) y[i] = static_cast<__bf16>(x[i]);
+    }
+  }
+}
+
 inline unsigned grid_for(int64_t n, int bs = 256) {
   int64_t g = cdiv(n, bs);
   if (g > 8192) g = 8192;
@@ -239,6 +269,27 @@ extern "C" int comet_cast(int dtype_in, int dtype_out, const void* x, void* y, i
   else
     hipLaunchKernelGGL((cast_kernel<__bf16, __bf16>), dim3(g), dim3(256), 0, s, (const __bf16*)x, (__bf16*)y, n);
   COMET_CHECK_LAUNCH("comet_cast");
+  return COMET_OK;
+}
+
+extern "C" int comet_cast_multi_f32_bf16(const float* const* src, void* const* dst, const int64_t* sizes,
+                                         int n_tensors, void* stream) {
+  COMET_CHECK_ARG(n_tensors >= 0 && (n_tensors == 0 || (src && dst && sizes)), "comet_cast_multi_f32_bf16: bad args");
+  hipStream_t s = as_stream(stream);
+  for (int base = 0; base < n_tensors; base += CAST_MAX) {
+    CastPtrs cp{};
+    cp.count = n_tensors - base < CAST_MAX ? n_tensors - base : CAST_MAX;
+    int64_t total = 0;
+    for (int i = 0; i < cp.count; ++i) {
+      COMET_CHECK_ARG(src[base + i] && dst[base + i] && sizes[base + i] >= 0, "comet_cast_multi_f32_bf16: null tensor");
+      cp.s[i] = src[base + i];
+      cp.d[i] = reinterpret_cast<__bf16*>(dst[base + i]);
+      cp.n[i] = sizes[base + i];
+      total += cp.n[i];
+    }
+    hipLaunchKernelGGL(cast_multi_kernel, dim3(grid_for(total / 4 + 1)), dim3(256), 0, s, cp);
+    COMET_CHECK_LAUNCH("comet_cast_multi_f32_bf16");
+  }
   return COMET_OK;
 }
 

@@ -199,6 +199,10 @@ int comet_attn_dsoftmax(int dtype_p, const void* p, const void* dp, const float*
  * Elementwise / reductions.
  * ------------------------------------------------------------------------------------- */
 int comet_cast(int dtype_in, int dtype_out, const void* x, void* y, int64_t n, void* stream);
+/* dst[i][0:sizes[i]] = bf16(src[i][...]) for n_tensors f32 tensors in few launches (the bf16
+ * copies of the trainable camera-head weights, refreshed after each AdamW step). */
+int comet_cast_multi_f32_bf16(const float* const* src, void* const* dst, const int64_t* sizes,
+                              int n_tensors, void* stream);
 /* y = act(x) (f32 or bf16); gelu backward: dx = dy * gelu'(pre) */
 int comet_act_bwd(int act, int dtype_pre, int dtype_dy, const void* pre, const void* dy,
                   void* dx, int dtype_dx, int64_t n, void* stream);

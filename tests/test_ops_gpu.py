@@ -777,3 +777,25 @@ def test_sq_norm_multi_vectorised_and_ragged():
     L.check(L.load().comet_sq_norm_multi(arr, sz, len(views), out.data_ptr(), ops.stream()), "sq_norm")
     ref = sum((v.double().cpu() ** 2).sum() for v in views)
     _close(out, ref.reshape(1), 1e-5, 0, "sq_norm_multi")
+
+
+def test_cast_multi_and_weight_cache_refresh():
+    """comet_cast_multi_f32_bf16 equals torch's RNE .to(bfloat16) bit for bit (aligned and
+    unaligned views, > 48 tensors); refresh_weight_cache re-casts cached copies in place after
+    the parameters change."""
+    from comet_amd import functional as Fn
+    from comet_amd import ops
+    base = _rand(200_000, seed=200).to(DEV)
+    srcs = [base[1:1 + 999], base[1024:1024 + 4096], base[9000:9000 + 7]] + [base[10000 + 64 * i:10000 + 64 * i + 33 + i] for i in range(60)]
+    dsts = [torch.empty(s.numel(), device=DEV, dtype=torch.bfloat16) for s in srcs]
+    ops.cast_multi_f32_bf16(srcs, dsts)
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(d, s.to(torch.bfloat16))
+    w = torch.nn.Parameter(_rand(384, 96, seed=201).to(DEV))
+    c_full, c_top = Fn.wcast(w), Fn.wcast(w[:128])
+    with torch.no_grad():
+        w.mul_(1.5).add_(0.25)
+    Fn.refresh_weight_cache([w])
+    assert Fn.wcast(w) is c_full and torch.equal(c_full, w.detach().to(torch.bfloat16))
+    assert torch.equal(Fn.wcast(w[:128]), w.detach()[:128].to(torch.bfloat16))
+    Fn.invalidate_weight_cache([w])
