@@ -1503,7 +1503,9 @@ Plan make_plan(const comet_gemm_args& a) {
     } else {
       const int64_t tiles = cdiv(a.m, big::BM) * cdiv(a.n, bn), ktiles = a.k / 64;
       if (tiles < kCUs && ktiles >= 16) {
-        int64_t s2 = cdiv(2 * kCUs, tiles);
+        // one full round of workgroups (one 256-row workgroup per CU): 36 dW tiles x 7 splits run
+        // K/7 per CU, where ~2 rounds (x 15) ran 3 rounds of K/15 and doubled the partials
+        int64_t s2 = kCUs / tiles;
         if (s2 > ktiles / 8) s2 = ktiles / 8;
         if (s2 > 64) s2 = 64;
         sp = s2 < 1 ? 1 : (int)s2;
