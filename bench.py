@@ -145,7 +145,7 @@ def main():
     cfg = load_config()
     torch.manual_seed(0)  # identical random-init weights on every rank
     model = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg).to(dev)
-    opt, sched = build_optimizer(cfg, model, iters_per_epoch=1000)
+    opt, sched = build_optimizer(cfg, model, 1000)
     ddp = GradBucketer(model.camera_predictor.parameters()) if world > 1 else None
     B, T = args.batch, args.frames
     img, tracks, cams = synthetic(B, T, args.image, args.tracks, dev, seed=1 + rank)

@@ -3,83 +3,128 @@ DistributedDataParallel, train_e2epose2.py:83).
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI). Sequences shard over
 ranks; the only exchange is the average of the camera-predictor gradients (115.9 M f32 values,
-463.8 MB). Gradients live in flat buckets (~bucket_mb each, reverse registration order so the
-first buckets to complete are the head's last layers); each param's .grad is a view into its
-bucket, a post-accumulate-grad hook counts arrivals and launches an async all-reduce as soon as a
-bucket is complete, overlapping RCCL with the rest of the backward. Parameters that receive no
-gradient (the reference's unused modules) keep .grad = None afterwards, so AdamW skips them as
-torch does; their (zero) slots are reduced with the last incomplete buckets.
+463.8 MB). Gradients live in flat f32 buckets (~25 MB); each param's .grad is a view into its
+bucket and a post-accumulate-grad hook counts arrivals and launches an async all-reduce
+(ReduceOp.AVG) as soon as its bucket is complete, overlapping RCCL with the rest of the backward.
+
+Bucket layout (what torch DDP does with find_unused_parameters + bucket rebuilding):
+  * step 1 ("discovery"): one provisional layout over every trainable param in reverse
+    registration order; all buckets are reduced at finish_backward. The hooks record the order in
+    which gradients arrive.
+  * afterwards the buckets are rebuilt over the params that did receive a gradient, in rank 0's
+    arrival order (broadcast once, so every rank cuts identical buckets). The reference's 2.28 M
+    never-executed params (FeatureFusion, motion encoders, ...) are excluded, so no bucket waits
+    on a gradient that never comes: each bucket's all-reduce starts during the backward.
+    Excluded params keep .grad = None, so AdamW skips them as torch does.
+`static_used` (the params that receive gradients, in bucket order) skips discovery when the set is
+known up front.
 """
 import torch
 import torch.distributed as dist
 
 
 class GradBucketer:
-    def __init__(self, params, bucket_mb=64, group=None):
+    def __init__(self, params, bucket_mb=25, group=None, static_used=None):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.backend = dist.get_backend(group) if dist.is_initialized() else None
-        cap = int(bucket_mb * 1024 * 1024 // 4)
-        self.buckets = []  # list of (flat tensor, [(param, offset, numel)])
+        self.cap = max(1, int(bucket_mb * 1024 * 1024 // 4))
+        self.index = {p: i for i, p in enumerate(self.params)}
+        self.discovering = static_used is None
+        order = list(reversed(self.params)) if static_used is None else list(static_used)
+        self._build(order)
+        self.arrival = []
+        self.launch_log = []  # (bucket, during_backward) of the last step, for tests / tracing
+        self.in_backward = False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    # ---------------------------------------------------------------------------------------
+    def _build(self, order):
+        self.buckets = []
         cur, size = [], 0
-        for p in reversed(self.params):
-            if cur and size + p.numel() > cap:
+        for p in order:
+            if cur and size + p.numel() > self.cap:
                 self.buckets.append(cur)
                 cur, size = [], 0
             cur.append(p)
             size += p.numel()
         if cur:
             self.buckets.append(cur)
-        self.flat = []
-        self.slot = {}
+        self.flat, self.slot = [], {}
         for bi, plist in enumerate(self.buckets):
             n = sum(p.numel() for p in plist)
-            buf = torch.zeros(n, device=plist[0].device, dtype=torch.float32)
+            self.flat.append(torch.zeros(n, device=plist[0].device, dtype=torch.float32))
             off = 0
             for p in plist:
                 self.slot[p] = (bi, off)
                 off += p.numel()
-            self.flat.append(buf)
-        self.pending = [0] * len(self.buckets)
-        self.launched = [False] * len(self.buckets)
-        self.works = []
-        self.arrived = set()
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    def _rebuild_from_arrival(self):
+        idx = torch.tensor([self.index[p] for p in self.arrival], dtype=torch.int64)
+        if self.world > 1:
+            n = torch.tensor([idx.numel()], dtype=torch.int64)
+            dev = self.flat[0].device if self.backend == "nccl" else torch.device("cpu")
+            n = n.to(dev)
+            dist.broadcast(n, 0, group=self.group)
+            buf = torch.zeros(int(n.item()), dtype=torch.int64, device=dev)
+            if dist.get_rank(self.group) == 0:
+                buf.copy_(idx.to(dev))
+            dist.broadcast(buf, 0, group=self.group)
+            idx = buf.cpu()
+        used = [self.params[i] for i in idx.tolist()]
+        grads = {p: p.grad for p in used}
+        self._build(used)
+        for p in used:  # keep this step's reduced values in the new layout
+            v = self._view(p)
+            if grads[p] is not None:
+                v.copy_(grads[p])
+            p.grad = v
+        self.discovering = False
 
     def _view(self, p):
         bi, off = self.slot[p]
         return self.flat[bi][off:off + p.numel()].view_as(p)
 
+    # ---------------------------------------------------------------------------------------
     def prepare_backward(self):
         for buf in self.flat:
             buf.zero_()
         for p in self.params:
-            p.grad = self._view(p)
+            p.grad = self._view(p) if p in self.slot else None
         self.pending = [len(pl) for pl in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.works = []
         self.arrived = set()
+        self.arrival = []
+        self.launch_log = []
+        self.in_backward = True
 
     def _launch(self, bi):
         if self.launched[bi]:
             return
         self.launched[bi] = True
+        self.launch_log.append((bi, self.in_backward))
         if self.world == 1:
             return
         op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
         self.works.append((bi, dist.all_reduce(self.flat[bi], op=op, group=self.group, async_op=True)))
 
     def _on_grad(self, p):
-        if p in self.arrived or p not in self.slot:
+        if p in self.arrived:
             return
         self.arrived.add(p)
+        self.arrival.append(p)
+        if p not in self.slot:
+            raise RuntimeError("GradBucketer: a parameter that received no gradient in the discovery step now "
+                               "has one (the graph changed); build the bucketer with static_used")
         bi = self.slot[p][0]
         self.pending[bi] -= 1
-        if self.pending[bi] == 0:
+        if self.pending[bi] == 0 and not self.discovering:
             self._launch(bi)
 
     def finish_backward(self):
+        self.in_backward = False
         for bi in range(len(self.buckets)):
             self._launch(bi)
         for bi, w in self.works:
@@ -89,6 +134,8 @@ class GradBucketer:
         for p in self.params:
             if p not in self.arrived:
                 p.grad = None
+        if self.discovering:
+            self._rebuild_from_arrival()
 
     def remove(self):
         for h in self._hooks:

@@ -53,15 +53,19 @@ def wcast(p, dt=None):
         return p
     key = (p.data_ptr(), tuple(p.shape), tuple(p.stride()), dt)
     hit = _wcache.get(key)
-    if hit is not None:
+    # an in-place write through torch (load_state_dict, copy_) bumps the version counter the
+    # detached source shares; the optimizer's raw-pointer update re-casts via refresh_weight_cache
+    if hit is not None and _wver.get(key) == p._version:
         return hit
     c = ops.cast(p.detach(), dt)
     _wcache[key] = c
-    _wsrc[key] = p.detach()
+    _wsrc[key] = p.detach()  # pins the source storage: its address cannot be reused while cached
+    _wver[key] = p._version
     return c
 
 
 _wsrc = {}
+_wver = {}
 
 
 def refresh_weight_cache(params):
@@ -84,6 +88,7 @@ def refresh_weight_cache(params):
         else:
             del _wcache[k]
             _wsrc.pop(k, None)
+            _wver.pop(k, None)
     if src:
         ops.cast_multi_f32_bf16(src, dst)
 
@@ -93,6 +98,7 @@ def invalidate_weight_cache(params=None):
     if params is None:
         _wcache.clear()
         _wsrc.clear()
+        _wver.clear()
         return
     spans = [(p.data_ptr(), p.data_ptr() + p.numel() * p.element_size()) for p in params]
 
@@ -101,6 +107,7 @@ def invalidate_weight_cache(params=None):
     for k in [k for k in _wcache if any(lo <= ptr(k) < hi for lo, hi in spans)]:
         del _wcache[k]
         _wsrc.pop(k, None)
+        _wver.pop(k, None)
 
 
 def _needs_grad(*ts):
@@ -533,7 +540,7 @@ def wcast_conv(w, k_align=8, cin_pad=None):
     cp = cin_pad or cin
     key = ("conv", w.data_ptr(), tuple(w.shape), dt, cp)
     hit = _wcache.get(key)
-    if hit is not None:
+    if hit is not None and _wver.get(key) == w._version:
         return hit
     K = cp * kh * kw
     Kp = (K + k_align - 1) // k_align * k_align
@@ -542,4 +549,6 @@ def wcast_conv(w, k_align=8, cin_pad=None):
     wp[..., :cin] = w.detach().permute(0, 2, 3, 1).to(dt)
     wm[:, :K] = wp.reshape(cout, K)
     _wcache[key] = wm
+    _wver[key] = w._version
+    _wsrc[key] = w.detach()  # pins the source storage: its address cannot be reused while cached
     return wm

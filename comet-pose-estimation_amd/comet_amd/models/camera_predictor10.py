@@ -123,6 +123,8 @@ class CameraPredictor(nn.Module):
         self.fc_translation2d = nn.Linear(768, 2)
         self.fc_depth = nn.Linear(768, 1)
         self._tables = {}
+        # compute only the rows of the last attention layer that reach the output (same result)
+        self.prune_dead_rows = True
 
     def get_backbone(self, backbone):
         if backbone == "dinov2b":
@@ -163,12 +165,45 @@ class CameraPredictor(nn.Module):
         tok = torch.cat([self.pose_token.expand(B, S, -1, -1), tok], dim=-2)
         P = P + 1
         for idx in range(self.att_depth):
+            if idx == self.att_depth - 1 and S > 1 and self.prune_dead_rows:
+                return self._last_layer_token0(tok, B, S, P, C), B, S, C
             tok = self.self_att[idx](tok.reshape(B * S, P, C)).reshape(B, S, P, C)
             f0 = tok[:, 0]
             fo = tok[:, 1:].reshape(B, (S - 1) * P, C)
             fo = self.cross_att[idx](fo, f0).reshape(B, S - 1, P, C)
             tok = torch.cat([tok[:, 0:1], fo], dim=1)
         return tok[:, :, 0].contiguous(), B, S, C
+
+    def _last_layer_token0(self, tok, B, S, P, C):
+        """The last (self_att, cross_att) pair computing only the rows that survive (SURVEY
+        Appendix B-8, camera_predictor10.py:666-687): only token 0 of every frame is returned, so
+          * self_att on frames 1..S-1 needs query row 0 only (keys / values still from all P rows);
+          * frame 0 keeps every row (all P are the cross-attention context);
+          * cross_att needs the S-1 query rows that are token 0 of frames 1..S-1.
+        Every surviving row goes through exactly the reference's per-row arithmetic (attention
+        query rows, LayerNorm, out_proj, Mlp are row-independent), so the result is the same. Per sequence at
+        T=16 this drops ~0.23 of the 5.15 TFLOP forward and ~0.47 of the 2.32 TFLOP backward
+        (the reported GFLOP/seq stays the reference's). -> rgb_feat [B, S, C]."""
+        blk, cblk = self.self_att[-1], self.cross_att[-1]
+        a = blk.attn
+        x = tok.reshape(B * S, P, C)
+        xn, xc = F.layer_norm_dual(x, eps=1e-6)  # every row: K / V need all of them
+        W, b = a.in_proj_weight, a.in_proj_bias
+        kv = F.linear(xc, W[C:], b[C:])  # [B*S, P, 2C]
+        xc4, xn4 = xc.reshape(B, S, P, C), xn.reshape(B, S, P, C)
+        # query rows: frame 0 (all P) then token 0 of every frame (frame 0's again: 1 row / sequence)
+        qin = torch.cat([xc4[:, 0].reshape(B * P, C), xc4[:, :, 0].reshape(B * S, C)])
+        rin = torch.cat([xn4[:, 0].reshape(B * P, C), xn4[:, :, 0].reshape(B * S, C)])
+        q = F.linear(qin, W[:C], b[:C])
+        o0 = F.attention(q[:B * P].reshape(B, P, C), kv.reshape(B, S, P, 2 * C)[:, 0], blk.heads, C)
+        o1 = F.attention(q[B * P:].reshape(B * S, 1, C), kv, blk.heads, C)
+        o = torch.cat([o0.reshape(B * P, C), o1.reshape(B * S, C)])
+        y = F.linear(o, a.out_proj.weight, a.out_proj.bias, resid=rin, out_dtype=torch.float32)
+        y = blk.mlp(F.layer_norm(y, eps=1e-6, out_dtype=F.compute_dtype()), resid=y)
+        f0 = y[:B * P].reshape(B, P, C)
+        rows = y[B * P:].reshape(B, S, C)[:, 1:].contiguous()
+        r = cblk(rows, f0)  # [B, S-1, C]
+        return torch.cat([f0[:, 0:1], r], dim=1)
 
     def forward(self, reshaped_image, preliminary_cameras=None, iters=4, batch_size=None, rgb_feat_init=None,
                 gt_cameras=None, fmaps=None, pred_trajectories=None, track_confidence=None, debug=False):
@@ -216,10 +251,9 @@ class CameraPredictor(nn.Module):
 
 
 def _ratio(cams):
-    r = cams.ratio
-    if torch.is_tensor(r):
-        return float(r.reshape(-1)[0].item())
-    return float(r)
+    """gt_cameras.ratio as the reference divides by it (a collated float64 tensor, B-15); handed to
+    the pose codec as is (ops._ratio_args: host value or device pointer, never a device sync)."""
+    return cams.ratio
 
 
 def _dataset(cfg):

@@ -38,21 +38,38 @@ class QuaternionCameras:
             pp = torch.as_tensor(principal_point, dtype=torch.float32, device=device)
             self.principal_point = pp.expand(N, 2) if pp.dim() == 1 else pp
 
+    def get_world_to_view_transform(self):
+        """train_eval_func_new_cp5.py:72-79."""
+        return _world_to_view(self)
+
 
 class PredCameras:
-    """Output cameras of pose_encoding_to_camera2 (R quaternion, T float64, focal [N, 0])."""
+    """Output cameras of pose_encoding_to_camera2 (utils.py:397-403), i.e. the reference's
+    train_eval_func.QuaternionCameras (train_eval_func.py:112-168): R [N,4] quaternion (w,x,y,z),
+    T [N,3] (float64, B-15), focal_length [N,0] (the 7-column encoding has no focal column),
+    principal_point zeros [N,2]."""
 
-    def __init__(self, R, T, focal_length):
+    def __init__(self, R, T, focal_length, principal_point=None):
         self.R = R
         self.T = T
         self.focal_length = focal_length
         self.device = R.device
+        N = R.shape[0]
+        self.principal_point = (torch.zeros((N, 2), device=R.device) if principal_point is None
+                                else principal_point)
+
+    def __repr__(self):
+        return (f"QuaternionCameras(batch={self.R.shape[0]}, device={self.device})\n"
+                f"  q: {self.R.shape}, T: {self.T.shape}\n"
+                f"  focal_length: {self.focal_length.shape}, principal_point: {self.principal_point.shape}")
 
     def get_world_to_view_transform(self):
-        from ..minipytorch3d.rotation_conversions import quaternion_to_matrix
-        Rm = quaternion_to_matrix(self.R)
-        M = torch.zeros(self.R.shape[0], 4, 4, dtype=Rm.dtype, device=Rm.device)
-        M[:, :3, :3] = Rm
-        M[:, 3, :3] = self.T.to(Rm.dtype)
-        M[:, 3, 3] = 1.0
-        return M
+        """train_eval_func.py:162-168: Transform3d with get_matrix() == [[R(q), 0], [T, 1]] (f32)."""
+        return _world_to_view(self)
+
+
+def _world_to_view(cams):
+    from ..minipytorch3d.rotation_conversions import quaternion_to_matrix
+    from ..minipytorch3d.transform3d import get_world_to_view_transform
+    cams.R_matrix = quaternion_to_matrix(cams.R)
+    return get_world_to_view_transform(R=cams.R_matrix, T=cams.T)

@@ -534,10 +534,23 @@ def sincos_2d(embed_dim, gh, gw, device):
     return out
 
 
+def _ratio_args(ratio):
+    """(host value, device pointer or None): a ratio already in HBM (float64 tensor) is read by the
+    kernel, a host float / CPU tensor (the DataLoader's collated float64) is passed by value --
+    neither path synchronises the device."""
+    if torch.is_tensor(ratio):
+        if ratio.is_cuda:
+            r = ratio.reshape(-1)[:1].to(torch.float64).contiguous()
+            return 0.0, r, _p(r)
+        return float(ratio.reshape(-1)[0]), None, None
+    return float(ratio), None, None
+
+
 def pose_encode(R, T_uvz, focal, ratio, B, S):
     enc = torch.empty(B * S, 8, device=R.device, dtype=torch.float32)
+    rh, keep, rd = _ratio_args(ratio)
     _chk(L.load().comet_pose_encode(_p(R.contiguous()), _p(T_uvz.contiguous()), _p(focal.contiguous()),
-                                    float(ratio), _p(enc), B, S, stream()), "pose_encode")
+                                    rh, rd, _p(enc), B, S, stream()), "pose_encode")
     return enc
 
 
@@ -545,7 +558,8 @@ def pose_decode(enc, R_gt, T_gt, ratio, intr, B, S):
     Rout = torch.empty(B * S, 4, device=enc.device, dtype=torch.float32)
     Tout = torch.empty(B * S, 3, device=enc.device, dtype=torch.float64)
     fx, fy, cx, cy = intr
-    _chk(L.load().comet_pose_decode(_p(enc.contiguous()), _p(R_gt.contiguous()), _p(T_gt.contiguous()), float(ratio),
+    rh, keep, rd = _ratio_args(ratio)
+    _chk(L.load().comet_pose_decode(_p(enc.contiguous()), _p(R_gt.contiguous()), _p(T_gt.contiguous()), rh, rd,
                                     fx, fy, cx, cy, _p(Rout), _p(Tout), B, S, stream()), "pose_decode")
     return Rout, Tout
 

@@ -150,8 +150,10 @@ __device__ __forceinline__ void qmul_std(const float* a, const float* b, float* 
 
 // camera_to_pose_encoding2 per frame (per-sequence reference = frame 0 of each sequence)
 __global__ void pose_encode_kernel(const float* __restrict__ R, const float* __restrict__ T,
-                                   const float* __restrict__ focal, double ratio, float* __restrict__ enc,
+                                   const float* __restrict__ focal, double ratio,
+                                   const double* __restrict__ ratio_dev, float* __restrict__ enc,
                                    int64_t B, int S) {
+  if (ratio_dev) ratio = *ratio_dev;
   GRID_STRIDE(t, B * S) {
     const int64_t b = t / S;
     const int s = (int)(t % S);
@@ -182,9 +184,11 @@ __global__ void pose_encode_kernel(const float* __restrict__ R, const float* __r
 // pose_encoding_to_camera2 per frame: enc [B*S, 7]; reference = frame 0 of each sequence's gt.
 // T is produced in double (the reference promotes through the float64 `ratio`, B-15).
 __global__ void pose_decode_kernel(const float* __restrict__ enc, const float* __restrict__ Rgt,
-                                   const float* __restrict__ Tgt, double ratio, double fx, double fy,
+                                   const float* __restrict__ Tgt, double ratio,
+                                   const double* __restrict__ ratio_dev, double fx, double fy,
                                    double cx, double cy, float* __restrict__ Rout, double* __restrict__ Tout,
                                    int64_t B, int S) {
+  if (ratio_dev) ratio = *ratio_dev;
   GRID_STRIDE(t, B * S) {
     const int64_t b = t / S;
     const float* e = enc + t * 7;
@@ -392,20 +396,20 @@ extern "C" int comet_harmonic_bwd(const float* x, const float* diag_cov, const f
 }
 
 extern "C" int comet_pose_encode(const float* R, const float* T_uvz, const float* focal, double ratio,
-                                 float* enc, int64_t B, int S, void* stream) {
+                                 const double* ratio_dev, float* enc, int64_t B, int S, void* stream) {
   COMET_CHECK_ARG(R && T_uvz && focal && enc && S >= 1, "comet_pose_encode: bad args");
   hipLaunchKernelGGL(pose_encode_kernel, dim3(g1d(B * S)), dim3(256), 0, as_stream(stream), R, T_uvz, focal,
-                     ratio, enc, B, S);
+                     ratio, ratio_dev, enc, B, S);
   COMET_CHECK_LAUNCH("comet_pose_encode");
   return COMET_OK;
 }
 
 extern "C" int comet_pose_decode(const float* enc, const float* R_gt, const float* T_uvz_gt, double ratio,
-                                 double fx, double fy, double cx, double cy, float* R_out, double* T_out,
+                                 const double* ratio_dev, double fx, double fy, double cx, double cy, float* R_out, double* T_out,
                                  int64_t B, int S, void* stream) {
   COMET_CHECK_ARG(enc && R_gt && T_uvz_gt && R_out && T_out, "comet_pose_decode: bad args");
   hipLaunchKernelGGL(pose_decode_kernel, dim3(g1d(B * S)), dim3(256), 0, as_stream(stream), enc, R_gt, T_uvz_gt,
-                     ratio, fx, fy, cx, cy, R_out, T_out, B, S);
+                     ratio, ratio_dev, fx, fy, cx, cy, R_out, T_out, B, S);
   COMET_CHECK_LAUNCH("comet_pose_decode");
   return COMET_OK;
 }

@@ -283,12 +283,15 @@ int comet_harmonic_bwd(const float* x, const float* diag_cov, const float* freqs
                        float* dx, float* dcov, int64_t rows, int dim, int n_freqs, int append_input,
                        void* stream);
 /* camera_to_pose_encoding2 per sequence (utils.py:631-688): R [B*S,4], T_uvz [B*S,3],
- * focal [B*S,2] -> enc [B*S,8]; ratio as in the reference (float64). */
-int comet_pose_encode(const float* R, const float* T_uvz, const float* focal, double ratio, float* enc,
-                      int64_t B, int S, void* stream);
+ * focal [B*S,2] -> enc [B*S,8]; ratio as in the reference (float64): the host value, or, when
+ * ratio_dev is non-NULL, the float64 read from that device address (no host sync for a ratio that
+ * already lives in HBM). */
+int comet_pose_encode(const float* R, const float* T_uvz, const float* focal, double ratio,
+                      const double* ratio_dev, float* enc, int64_t B, int S, void* stream);
 /* pose_encoding_to_camera2 per sequence (utils.py:312-403): enc [B*S,7] -> R [B*S,4] (f32),
  * T [B*S,3] (f64, as the reference's float64 promotion), intrinsics fx, fy, cx, cy. */
-int comet_pose_decode(const float* enc, const float* R_gt, const float* T_uvz_gt, double ratio, double fx,
+int comet_pose_decode(const float* enc, const float* R_gt, const float* T_uvz_gt, double ratio,
+                      const double* ratio_dev, double fx,
                       double fy, double cx, double cy, float* R_out, double* T_out, int64_t B, int S,
                       void* stream);
 /* GAPR head + pose loss (camera_predictor10.py:385-460): F.normalize(rot, eps 1e-8), loss =

@@ -1,0 +1,191 @@
+"""Correctness at the BASELINE configs that are not the headline one.
+
+configs[4] (long-sequence stress, B=4, T=64, 768x768, N=512, bf16): at this size the fine feature
+map [B*N*T, 31, 31, 32] holds 4.03e9 elements (> 2^31), so any 32-bit flat offset into it would
+corrupt sequences 2-3 silently. Size-independent property: every sequence of the B=4 run equals the
+same sequence run alone (B=1, 1.0e9 elements < 2^31) -- processing is per sequence (SURVEY
+Appendix B-1). The cross-frame attention at this size (Lq = 63 x 577 = 36351 queries, Lk = 577) is
+checked against an f64 reference on sampled rows.
+
+configs[3] (DDP, global batch over ranks): two ranks on this one GPU (gloo process group on device
+tensors), each running the real model on its own sequence; after GradBucketer's all-reduce
+(average) every rank's camera-predictor gradients equal the single-process B=2 gradients
+(SURVEY §4 "simulated ranks")."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _model():
+    from comet_amd.config import instantiate, load_config
+    from oracle import prng
+    from oracle.weights import comet_shapes
+    cfg = load_config()
+    torch.manual_seed(0)
+    m = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg)
+    m.load_state_dict(prng.make_state_dict(0, comet_shapes()), strict=True)
+    return m.cuda(), cfg
+
+
+def _cams(gt):
+    from comet_amd.models.utils import QuaternionCameras
+    return QuaternionCameras(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+                             principal_point=gt["principal_point"], ratio=gt["ratio"], device="cuda")
+
+
+def _sub(gt, b, T):
+    return {k: (v[b * T:(b + 1) * T] if k not in ("ratio",) else v) for k, v in gt.items()}
+
+
+def test_stress_B4_T64_768_sequences_independent_of_batch():
+    from comet_amd import functional as F
+    from oracle import prng
+    model, cfg = _model()
+    B, T, S, N = 4, 64, 768, 512
+    img, tracks, gt = prng.synthetic_batch(5, B, T, S, S, N)
+    img, tracks = img.cuda(), tracks.cuda()
+    P = 2 * 15 + 1
+    assert B * N * T * P * P * 32 > 2 ** 31
+    with F.precision(torch.bfloat16), torch.no_grad():
+        out = model(img, gt_cameras=_cams(gt), training=True, tracks=tracks)
+        enc4 = out["pred_pose_enc"].reshape(B, T, 7).float().cpu()
+        tr4 = out["pred_tracks"].float().cpu()
+        sc4 = out["_track_predictions"]["pred_score"].float().cpu()
+        del out
+        torch.cuda.empty_cache()
+        for b in (3, 2):
+            o1 = model(img[b:b + 1], gt_cameras=_cams(_sub(gt, b, T)), training=True, tracks=tracks[b:b + 1])
+            d_tr = (o1["pred_tracks"].float().cpu()[0] - tr4[b]).abs()
+            d_enc = (o1["pred_pose_enc"].float().cpu() - enc4[b]).abs().max().item()
+            d_sc = (o1["_track_predictions"]["pred_score"].float().cpu()[0] - sc4[b]).abs()
+            frac = float((d_tr > 1e-2).float().mean())
+            print(f"sequence {b}: tracks max diff {d_tr.max().item():.3e} (frac > 1e-2: {frac:.2e}), "
+                  f"score max diff {d_sc.max().item():.3e}, pose enc max diff {d_enc:.3e}")
+            # identical per-sequence work: equal up to bf16 reduction-order effects
+            assert frac < 1e-3, f"sequence {b}: {frac:.2e} of the tracks differ from the B=1 run"
+            assert float((d_sc > 1e-2).float().mean()) < 1e-3
+            assert d_enc < 1e-2
+            del o1
+    assert torch.isfinite(enc4).all() and torch.isfinite(tr4).all()
+
+
+def test_stress_cross_frame_attention_Lq36351_vs_f64():
+    """camera_predictor10.py:676-681: frames 1..63 (63 x 577 query tokens) attend frame 0 (577)."""
+    from comet_amd import functional as F
+    torch.manual_seed(3)
+    B, Lq, Lk, C, H = 4, 63 * 577, 577, 768, 8
+    q = torch.randn(B, Lq, C, device="cuda").to(torch.bfloat16)
+    kv = torch.randn(B, Lk, 2 * C, device="cuda").to(torch.bfloat16)
+    with F.precision(torch.bfloat16), torch.no_grad():
+        o = F.attention(q, kv, H, C)
+    torch.cuda.synchronize()
+    rows = torch.cat([torch.arange(0, 64), torch.randint(0, Lq, (448,)), torch.arange(Lq - 64, Lq)])
+    D = C // H
+    for b in (0, B - 1):
+        qq = q[b, rows].double().reshape(-1, H, D).transpose(0, 1)            # [H, r, D]
+        kk = kv[b, :, :C].double().reshape(Lk, H, D).transpose(0, 1)         # [H, Lk, D]
+        vv = kv[b, :, C:].double().reshape(Lk, H, D).transpose(0, 1)
+        ref = torch.softmax(qq @ kk.transpose(1, 2) * D ** -0.5, -1) @ vv     # [H, r, D]
+        ref = ref.transpose(0, 1).reshape(len(rows), C)
+        got = o[b, rows].double()
+        err = (got - ref).abs().max().item()
+        print(f"batch {b}: max err {err:.3e}")
+        assert err < 2e-2
+
+
+# ------------------------------------------------------------------------------------------
+# configs[3]: simulated ranks
+# ------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _inputs():
+    from oracle import prng
+    return prng.synthetic_batch(31, 2, 4, 128, 128, 16)
+
+
+def _rank(rank, world, port, q, paths):
+    import sys
+    sys.path[:0] = paths
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from comet_amd import functional as F
+        from comet_amd.ddp import GradBucketer
+        from comet_amd.train import build_optimizer
+        model, cfg = _model()
+        bk = GradBucketer(model.camera_predictor.parameters(), bucket_mb=25)
+        img, tracks, gt = _inputs()
+        res = []
+        for step in range(2):  # step 0 = bucket discovery, step 1 = rebuilt buckets with overlap
+            with F.precision(torch.float32):
+                out = model(img[rank:rank + 1].cuda(), gt_cameras=_cams(_sub(gt, rank, 4)), training=True,
+                            tracks=tracks[rank:rank + 1].cuda())
+                model.zero_grad(set_to_none=True)
+                bk.prepare_backward()
+                out["loss"].backward()
+                bk.finish_backward()
+            torch.cuda.synchronize()
+            res.append({k: p.grad.double().norm().item() for k, p in model.camera_predictor.named_parameters()
+                        if p.grad is not None})
+            g = {k: p.grad.detach().cpu().clone() for k, p in model.camera_predictor.named_parameters()
+                 if p.grad is not None and k in ("fc_depth.weight", "trunk.3.mlp.fc2.weight", "pose_token")}
+        during = all(d for _, d in bk.launch_log)
+        q.put((rank, res, g, during, len(bk.buckets)))
+        dist.destroy_process_group()
+    except Exception as e:  # surface the error to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc(), None, None))
+        raise
+
+
+def test_ddp_simulated_ranks_equal_B2_gradients():
+    from comet_amd import functional as F
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, [ROOT, PKG])) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2):
+        rank, res, g, during, nb = q.get(timeout=300)
+        assert res is not None, g
+        got[rank] = (res, g, during, nb)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process, B = 2
+    model, cfg = _model()
+    img, tracks, gt = _inputs()
+    with F.precision(torch.float32):
+        out = model(img.cuda(), gt_cameras=_cams(gt), training=True, tracks=tracks.cuda())
+        out["loss"].backward()
+    torch.cuda.synchronize()
+    ref = {k: p.grad for k, p in model.camera_predictor.named_parameters() if p.grad is not None}
+    for rank in (0, 1):
+        res, g, during, nb = got[rank]
+        assert during and nb > 1, "rebuilt buckets must all launch during the backward"
+        for step in (0, 1):
+            assert set(res[step]) == set(ref)
+            for k, n in res[step].items():
+                r = ref[k].double().norm().item()
+                assert abs(n - r) <= 1e-4 * r + 1e-7, (rank, step, k, n, r)
+        for k, v in g.items():
+            torch.testing.assert_close(v, ref[k].cpu(), rtol=1e-4, atol=1e-4 * ref[k].abs().max().item())

@@ -36,12 +36,23 @@ class _Net(torch.nn.Module):
         return self.c(torch.relu(self.b(torch.relu(self.a(x)))))
 
 
+class _NetUnusedLast(_Net):
+    """The never-executed module registered last: with reverse-registration buckets it sits in the
+    FIRST bucket (like the head's fc_depth ... pose_embed_scale block)."""
+
+    def __init__(self):
+        super().__init__()
+        del self.unused
+        torch.manual_seed(1)
+        self.unused = torch.nn.Linear(32, 8)
+
+
 def _data(rank, step):
     g = torch.Generator().manual_seed(100 * step + rank)
     return torch.randn(8, 16, generator=g), torch.randn(8, 4, generator=g)
 
 
-def _worker(rank, world, port, bucket_mb, q, paths):
+def _worker(rank, world, port, bucket_mb, q, paths, net_cls=_Net, steps=2):
     import sys
     sys.path[:0] = paths
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -49,25 +60,26 @@ def _worker(rank, world, port, bucket_mb, q, paths):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from comet_amd.ddp import GradBucketer
-        net = _Net()
+        net = net_cls()
         bk = GradBucketer(net.parameters(), bucket_mb=bucket_mb)
-        out = []
-        for step in range(2):
+        out, logs = [], []
+        for step in range(steps):
             bk.prepare_backward()
             x, y = _data(rank, step)
             loss = ((net(x) - y) ** 2).mean()
             loss.backward()
             bk.finish_backward()
             out.append({k: (None if p.grad is None else p.grad.detach().numpy().copy()) for k, p in net.named_parameters()})
-        q.put((rank, len(bk.buckets), out))
+            logs.append(list(bk.launch_log))
+        q.put((rank, len(bk.buckets), out, logs))
     finally:
         dist.destroy_process_group()
 
 
-def _expected(world):
-    net = _Net()
+def _expected(world, net_cls=_Net, steps=2):
+    net = net_cls()
     res = []
-    for step in range(2):
+    for step in range(steps):
         acc = {k: torch.zeros_like(p) for k, p in net.named_parameters()}
         for r in range(world):
             net.zero_grad(set_to_none=True)
@@ -91,7 +103,7 @@ def test_bucketed_allreduce_matches_mean_grad(bucket_mb):
         p.start()
     results = {}
     for _ in range(world):
-        rank, nb, out = q.get(timeout=120)
+        rank, nb, out, _ = q.get(timeout=120)
         results[rank] = (nb, out)
     for p in procs:
         p.join(timeout=60)
@@ -103,6 +115,41 @@ def test_bucketed_allreduce_matches_mean_grad(bucket_mb):
         for step in range(2):
             got = results[rank][1][step]
             for k, g in got.items():
+                if k.startswith("unused."):
+                    assert g is None, k
+                else:
+                    torch.testing.assert_close(torch.from_numpy(g), exp[step][k], rtol=1e-5, atol=1e-6)
+
+
+def test_unused_param_in_first_bucket_does_not_delay_allreduce():
+    """the never-executed params are excluded from the buckets after the discovery
+    step, so from step 2 on every bucket's all-reduce is launched during the backward (before
+    finish_backward), including the one that held the unused module in the provisional layout."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 0.004, q, [ROOT, PKG], _NetUnusedLast, 3))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        rank, nb, out, logs = q.get(timeout=120)
+        results[rank] = (nb, out, logs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = _expected(world, _NetUnusedLast, 3)
+    for rank in range(world):
+        nb, out, logs = results[rank]
+        assert nb > 1
+        assert all(not during for _, during in logs[0])          # discovery: reduced at finish
+        for step in (1, 2):
+            assert len(logs[step]) == nb and all(during for _, during in logs[step]), logs[step]
+            assert logs[step][0][0] == 0   # first bucket (the head's last layer) goes first
+        for step in range(3):
+            for k, g in out[step].items():
                 if k.startswith("unused."):
                     assert g is None, k
                 else:

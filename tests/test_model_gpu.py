@@ -213,3 +213,128 @@ def test_train_step_matches_oracle_adamw(setup):
         close(p.detach(), r, 1e-6, 1e-7, "AdamW param")
         p.data.copy_(b)  # restore for other tests
     F.invalidate_weight_cache()
+
+
+# ------------------------------------------------------------------------------------------
+# golden intermediates (v1) and round-2 fixtures (v2: pred_score, bf16 gradients, eval path)
+# ------------------------------------------------------------------------------------------
+GOLD2 = os.path.join(ROOT, "tests", "golden", "comet_golden_v2.npz")
+
+
+@pytest.fixture(scope="module")
+def gold2():
+    return dict(np.load(GOLD2, allow_pickle=False))
+
+
+def test_e2e_fp32_intermediates_match_reference(setup, gold):
+    """Stage outputs the reference golden already holds: coarse fmaps (BasicEncoder), fine patch
+    features (ShallowEncoder), DINOv2 patch tokens, first T_P cross-attention block, trunk output."""
+    model = setup[0]
+    cap = {}
+
+    def hook(name):
+        def f(m, i, o):
+            cap[name] = (o["x_norm_patchtokens"] if isinstance(o, dict) else o).detach().clone()
+        return f
+    cp, tp = model.camera_predictor, model.track_predictor
+    hs = [tp.coarse_fnet.register_forward_hook(hook("fmaps")), tp.fine_fnet.register_forward_hook(hook("patch")),
+          cp.backbone.register_forward_hook(hook("tokens")), cp.trunk[-1].register_forward_hook(hook("trunk")),
+          cp.cross_attn_block[0].register_forward_hook(hook("tp0"))]
+    try:
+        _run(setup, torch.float32)
+    finally:
+        for h in hs:
+            h.remove()
+    seed_w, seed_x, B, T, H, W, N = [int(v) for v in gold["cfg"]]
+    fm = cap["fmaps"].permute(0, 3, 1, 2)  # NHWC -> the reference's NCHW
+    ref = gold["e2e_fmaps"]
+    close(fm, ref, 1e-4, 1e-4 * float(np.abs(ref).max()), "coarse fmaps")
+    pf = cap["patch"]  # [(b n s), 31, 31, 32] -> the reference's [(b s n), 32, 31, 31]
+    P, C = pf.shape[1], pf.shape[-1]
+    pf = pf.reshape(B, N, T, P, P, C).permute(0, 2, 1, 5, 3, 4).reshape(B * T * N, C, P, P)
+    ref = gold["e2e_patch_feat_head"]
+    close(pf[:8], ref, 1e-4, 1e-4 * float(np.abs(ref).max()), "fine patch features (first 8)")
+    close(pf.double().sum().reshape(1), gold["e2e_patch_feat_sum"], 1e-4, 1e-2, "fine patch feature sum")
+    close(pf.double().abs().sum().reshape(1), gold["e2e_patch_feat_abssum"], 1e-5, 1e-2, "fine patch feature |sum|")
+    tok = cap["tokens"]
+    close(tok[:, :8], gold["e2e_tokens_head"], 1e-4, 1e-4, "DINOv2 patch tokens (first 8)")
+    close(tok.double().sum(dim=(1, 2)), gold["e2e_tokens_sum"], 1e-4, 1e-2, "DINOv2 token sums")
+    close(cap["tp0"], gold["e2e_tp0_out"], 1e-4, 1e-4, "T_P cross-attention block 0")
+    close(cap["trunk"], gold["e2e_trunk_out"], 1e-4, 1e-4, "T_F trunk output")
+
+
+def test_e2e_pred_score_matches_reference(setup, gold2):
+    out = _run(setup, torch.float32)
+    tp = out["_track_predictions"]
+    close(tp["pred_score"], gold2["e2e_pred_score"], 1e-4, 1e-5, "pred_score (inverted, normalised)")
+
+
+def test_e2e_bf16_grads_match_reference_bf16(setup, gold2):
+    """bf16 backward vs the reference's bf16-autocast backward (accelerate mixed_precision="bf16").
+    Both sides round GEMM operands to bf16 at different points, so gradients agree to bf16 accuracy:
+    norms within 5e-2 relative, elements within 5e-2 x max."""
+    model = setup[0]
+    out = _run(setup, torch.bfloat16, backward=True)
+    enc = out["pred_pose_enc"]
+    close(enc[:, :3], gold2["bf16_pred_pose_enc"][:, :3], 0, 1e-2, "uvz (bf16)")
+    close(enc[:, 3:], gold2["bf16_pred_pose_enc"][:, 3:], 0, 1e-2, "quaternion (bf16)")
+    named = dict(model.camera_predictor.named_parameters())
+    names = [str(k) for k in gold2["bf16_grad_names"]]
+    norms = np.array([named[k].grad.double().norm().item() for k in names])
+    close(norms, gold2["bf16_grad_norms"], 5e-2, 1e-4 * float(np.max(gold2["bf16_grad_norms"])), "bf16 grad norms")
+    for k in gold2:
+        if k.startswith("bf16_grad_full."):
+            ref = gold2[k]
+            close(named[k[len("bf16_grad_full."):]].grad, ref, 5e-2, 5e-2 * float(np.abs(ref).max()), k)
+    model.zero_grad(set_to_none=True)
+
+
+def test_eval_path_T16_matches_reference(setup, gold2):
+    """BASELINE configs[0]: abl_ours.py test_fn -> model(..., training=False), B=1, T=16
+    (E2Epose2.py:126-147), incl. the output cameras' world-to-view matrices (metric.py:155-156)."""
+    from comet_amd import functional as F
+    from comet_amd.models.utils import QuaternionCameras
+    from oracle import prng
+    model = setup[0]
+    seed_w, seed_x, B, T, H, W, N = [int(v) for v in gold2["eval_cfg"]]
+    img, tracks, gt = prng.synthetic_batch(seed_x, B, T, H, W, N)
+    cams = QuaternionCameras(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+                             principal_point=gt["principal_point"], ratio=gt["ratio"], device="cuda")
+    with F.precision(torch.float32):
+        out = model(img.cuda(), gt_cameras=cams, training=False, tracks=tracks.cuda())
+    torch.cuda.synchronize()
+    assert not out["pred_pose_enc"].requires_grad
+    close(out["pred_tracks"], gold2["eval_pred_tracks"], 1e-5, 1e-3, "eval tracks")
+    close(out["_track_predictions"]["pred_score"], gold2["eval_pred_score"], 1e-4, 1e-5, "eval pred_score")
+    enc = out["pred_pose_enc"]
+    close(enc[:, :3], gold2["eval_pred_pose_enc"][:, :3], 1e-4, 1e-4, "eval uvz")
+    close(enc[:, 3:], gold2["eval_pred_pose_enc"][:, 3:], 1e-4, 1e-4, "eval quaternion")
+    close(out["gt_pose_enc"], gold2["eval_gt_pose_enc"], 1e-6, 1e-6, "eval gt_pose_enc")
+    close(out["loss"].reshape(1), gold2["eval_loss"], 1e-4, 1e-5, "eval loss")
+    close(out["pred_cameras"].T, gold2["eval_pred_T"], 1e-4, 1e-3, "eval pred T")
+    M = out["pred_cameras"].get_world_to_view_transform().get_matrix()
+    close(M, gold2["eval_pred_w2v"], 1e-4, 1e-3, "eval pred world-to-view matrix")
+    close(cams.get_world_to_view_transform().get_matrix(), gold2["eval_gt_w2v"], 0, 1e-6, "eval gt world-to-view")
+    with pytest.raises(AssertionError):
+        model(torch.cat([img, img]).cuda(), gt_cameras=cams, training=False, tracks=torch.cat([tracks, tracks]).cuda())
+
+
+def test_dead_row_pruning_is_output_identical(setup):
+    """the last layer computes only the rows that reach token 0; outputs and
+    gradients equal the unpruned computation (fp32, golden configuration)."""
+    model = setup[0]
+    cp = model.camera_predictor
+    res = []
+    for prune in (False, True):
+        cp.prune_dead_rows = prune
+        out = _run(setup, torch.float32, backward=True)
+        res.append((out["pred_pose_enc"].detach().clone(), out["loss"].detach().clone(),
+                    {k: p.grad.detach().clone() for k, p in cp.named_parameters() if p.grad is not None}))
+    cp.prune_dead_rows = True
+    model.zero_grad(set_to_none=True)
+    (e0, l0, g0), (e1, l1, g1) = res
+    close(e1, e0.cpu(), 1e-5, 1e-6, "pose enc pruned vs full")
+    close(l1.reshape(1), l0.reshape(1).cpu(), 1e-5, 1e-6, "loss pruned vs full")
+    assert set(g0) == set(g1)
+    for k in g0:
+        close(g1[k], g0[k].cpu(), 1e-4, 1e-5 * float(g0[k].abs().max()) + 1e-12, f"grad {k} pruned vs full")

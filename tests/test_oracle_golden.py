@@ -139,3 +139,74 @@ def test_e2e_grads_match_reference(gold, e2e):
         if k.startswith("grad_full."):
             ref = gold[k]
             close(grads["camera_predictor." + k[len("grad_full."):]], ref, 2e-4, 2e-5 * float(np.abs(ref).max()), k)
+
+
+# ------------------------------------------------------------------------------------------
+# round-2 fixtures: eval path at T=16 (v2) and the headline workload, stage by stage
+# ------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def gold2():
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "comet_golden_v2.npz"), allow_pickle=False))
+
+
+@pytest.fixture(scope="module")
+def full_params():
+    from oracle.weights import comet_shapes
+    return prng.make_state_dict(0, comet_shapes())
+
+
+def test_eval_T16_matches_reference(gold2, full_params):
+    seed_w, seed_x, B, T, H, W, N = [int(v) for v in gold2["eval_cfg"]]
+    img, tracks, gt = prng.synthetic_batch(seed_x, B, T, H, W, N)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    with torch.no_grad():
+        out = O.comet_forward(full_params, img, tracks, gt, return_all=True)
+    close(out["pred_tracks"], gold2["eval_pred_tracks"], 1e-6, 1e-4, "eval tracks")
+    close(out["inv_score"], gold2["eval_pred_score"], 1e-5, 1e-6, "eval pred_score")
+    close(out["pred_pose_enc"], gold2["eval_pred_pose_enc"], 1e-5, 1e-5, "eval pose enc")
+    close(out["loss"].reshape(1), gold2["eval_loss"], 1e-5, 1e-6, "eval loss")
+    close(out["pred_T"], gold2["eval_pred_T"], 1e-5, 1e-4, "eval pred T")
+
+
+def test_small_pred_score_matches_reference(gold2, full_params):
+    gold1 = dict(np.load(GOLD, allow_pickle=False))
+    seed_w, seed_x, B, T, H, W, N = [int(v) for v in gold1["cfg"]]
+    img, tracks, gt = prng.synthetic_batch(seed_x, B, T, H, W, N)
+    with torch.no_grad():
+        out = O.comet_forward(full_params, img, tracks, gt, return_all=True)
+    close(out["score"], gold2["e2e_track_score"], 1e-5, 1e-6, "track score")
+    close(out["inv_score"], gold2["e2e_pred_score"], 1e-5, 1e-6, "pred_score")
+
+
+@pytest.fixture(scope="module")
+def headline():
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "comet_golden_headline.npz"), allow_pickle=False))
+    seed_w, seed_x, B, T, H, W, N = [int(v) for v in g["head_cfg"]]
+    img, tracks, gt = prng.synthetic_batch(seed_x, B, T, H, W, N)
+    return g, img, tracks, gt
+
+
+def test_headline_stages_match_reference(headline, full_params):
+    """T=16, 512^2, N=512 (the bench workload per sequence): coarse tracker from scratch, refine on
+    the reference's coarse tracks, camera predictor on the reference's refined tracks / scores."""
+    g, img, tracks, gt = headline
+    P = full_params
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    import torch.nn.functional as TF
+    B, T, C, H, W = img.shape
+    with torch.no_grad():
+        x = TF.interpolate(img.reshape(B * T, C, H, W), scale_factor=0.5, mode="bilinear", align_corners=True)
+        fm = O.basic_encoder(x, P, "track_predictor.coarse_fnet", 4)
+        fm = fm.reshape(B, T, -1, fm.shape[-2], fm.shape[-1])
+        preds = O.tracker_predictor(tracks[:, 0], fm, P, "track_predictor.coarse_predictor", 4, 4, 2, 5, 4, 128,
+                                    False, True)[0]
+        close(preds[-1], g["head_coarse"], 1e-6, 1e-3, "headline coarse tracks")
+        coarse = torch.from_numpy(g["head_coarse"])
+        refined, score = O.refine_track(img, P, coarse)
+        close(refined, g["head_refined"], 1e-6, 1e-3, "headline refined tracks")
+        close(score, g["head_score"], 1e-4, 1e-5, "headline score")
+        out = O.camera_predictor(img.reshape(-1, C, H, W), B, P, gt, torch.from_numpy(g["head_refined"]),
+                                 torch.from_numpy(g["head_pred_score"]))
+    close(out["pred_pose_enc"], g["head_pred_pose_enc"], 1e-5, 1e-5, "headline pose enc")
+    close(out["loss"].reshape(1), g["head_loss"], 1e-5, 1e-6, "headline loss")
+    close(out["pred_T"], g["head_pred_T"], 1e-5, 1e-4, "headline pred T")

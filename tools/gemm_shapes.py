@@ -27,7 +27,7 @@ def main():
     cfg = load_config()
     torch.manual_seed(0)
     model = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg).to(dev)
-    opt, sched = build_optimizer(cfg, model, iters_per_epoch=1000)
+    opt, sched = build_optimizer(cfg, model, 1000)
     img, tracks, cams = bench.synthetic(args.batch, 16, 512, 512, dev, seed=1)
     for it in range(2):
         if it == 1:

@@ -204,6 +204,215 @@ def gen_exact(out):
         out[f"codec_dec_T_{it}"] = np32(pc.T)
 
 
+CFG_EVAL = dict(B=1, T=16, H=128, W=128, N=16)
+
+
+def _capture_score(E2E):
+    """Wrap the reference's refine_track (as E2Epose2 imported it) to record track_score."""
+    cap = {}
+    orig = E2E.refine_track
+
+    def wrapped(*a, **k):
+        r = orig(*a, **k)
+        cap["score"] = r[1]
+        return r
+    E2E.refine_track = wrapped
+    return cap, orig
+
+
+def gen_v2(out):
+    """Round-2 fixtures (tests/golden/comet_golden_v2.npz):
+    * e2e (CFG_SMALL, fp32): the reference's predictions["pred_score"] (inverted, normalised score);
+    * e2e bf16 autocast: pose enc, loss and the camera-predictor gradients (norms + a few full);
+    * eval path (BASELINE configs[0] shape: abl_ours.py test_fn -> model(..., training=False), B=1,
+      T=16; frames 128^2, N=16): pose enc, tracks, loss, and get_world_to_view_transform().get_matrix()
+      of the predicted and GT cameras (metric.py:155-156, 219-221);
+    * WarmupCosineRestarts (train_util.py:2099-2128) lr sequences for three settings."""
+    E2E = H.reference_module("E2Epose2")
+    cap, orig = _capture_score(E2E)
+    try:
+        torch.manual_seed(0)
+        cfg = H.load_cfg()
+        model = H.build_reference_comet(cfg)
+        P, P_hf = reference_state(model, SEED_W)
+        model.load_state_dict(P_hf, strict=True)
+        QC = H.reference_module("train_eval_func_new_cp5").QuaternionCameras
+        q = CFG_SMALL
+        img, tracks, gt = prng.synthetic_batch(SEED_X, q["B"], q["T"], q["H"], q["W"], q["N"])
+        cams = QC(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+                  principal_point=gt["principal_point"], ratio=gt["ratio"])
+        vis = torch.ones(q["B"], q["T"], q["N"], dtype=torch.bool)
+        with torch.no_grad():
+            model(img, gt_cameras=cams, training=True, tracks=tracks, tracks_visibility=vis)
+        s = cap["score"]
+        inv = 1.0 / (s + 1e-6)
+        out["e2e_track_score"] = np32(s)
+        out["e2e_pred_score"] = np32(inv / inv.max(dim=1, keepdim=True)[0])
+        # bf16 autocast forward + backward (accelerate mixed_precision="bf16")
+        model.zero_grad()
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            pb = model(img, gt_cameras=cams, training=True, tracks=tracks, tracks_visibility=vis)
+        pb["loss"].float().mean().backward()
+        grads = {k: p.grad.float() for k, p in model.camera_predictor.named_parameters() if p.grad is not None}
+        names = sorted(grads)
+        out["bf16_grad_names"] = np.array(names)
+        out["bf16_grad_norms"] = np.array([grads[k].double().norm().item() for k in names])
+        for k in ["fc_depth.weight", "fc_translation2d.weight", "pose_branch.fc2.weight", "trunk.3.mlp.fc2.bias",
+                  "confidence_attention.0.weight"]:
+            out["bf16_grad_full." + k] = np32(grads[k])
+        out["bf16_pred_pose_enc"] = np32(pb["pred_pose_enc"].float())
+        out["bf16_loss"] = np32(pb["loss"].float().reshape(1))
+        model.zero_grad()
+        # eval path at T=16
+        e = CFG_EVAL
+        img, tracks, gt = prng.synthetic_batch(SEED_X + 20, e["B"], e["T"], e["H"], e["W"], e["N"])
+        cams = QC(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+                  principal_point=gt["principal_point"], ratio=gt["ratio"])
+        pe = model(img, gt_cameras=cams, training=False, tracks=tracks,
+                   tracks_visibility=torch.ones(e["B"], e["T"], e["N"], dtype=torch.bool))
+        out["eval_cfg"] = np.array([SEED_W, SEED_X + 20, e["B"], e["T"], e["H"], e["W"], e["N"]])
+        out["eval_pred_pose_enc"] = np32(pe["pred_pose_enc"])
+        out["eval_gt_pose_enc"] = np32(pe["gt_pose_enc"])
+        out["eval_pred_tracks"] = np32(pe["pred_tracks"])
+        out["eval_loss"] = np32(pe["loss"].reshape(1))
+        out["eval_pred_R"] = np32(pe["pred_cameras"].R)
+        out["eval_pred_T"] = pe["pred_cameras"].T.detach().double().cpu().numpy()
+        out["eval_pred_w2v"] = np32(pe["pred_cameras"].get_world_to_view_transform().get_matrix())
+        out["eval_gt_w2v"] = np32(cams.get_world_to_view_transform().get_matrix())
+        inv = 1.0 / (cap["score"] + 1e-6)
+        out["eval_pred_score"] = np32(inv / inv.max(dim=1, keepdim=True)[0])
+        # oracle cross-check on the eval inputs
+        res = O.comet_forward(P, img, tracks, dict(gt))
+        print("oracle vs reference (eval T=16):",
+              f"pose enc {(res['pred_pose_enc'] - pe['pred_pose_enc']).abs().max().item():.2e}",
+              f"tracks {(res['pred_tracks'] - pe['pred_tracks']).abs().max().item():.2e}")
+    finally:
+        E2E.refine_track = orig
+    # lr schedule
+    tu = _reference_train_util()
+    for tag, kw, n in [("a", dict(T_0=3, iters_per_epoch=4, warmup_ratio=0.25, warmup_lr_init=1e-7), 30),
+                       ("b", dict(T_0=320, iters_per_epoch=2, warmup_ratio=0.0, warmup_lr_init=1e-7), 50),
+                       ("c", dict(T_0=2, iters_per_epoch=3, T_mult=2, warmup_ratio=0.1, warmup_lr_init=1e-6,
+                                  eta_min=1e-7), 40)]:
+        opt = torch.optim.AdamW([torch.nn.Parameter(torch.zeros(1))], lr=1e-5)
+        sch = tu.WarmupCosineRestarts(opt, **kw)
+        lrs = []
+        for _ in range(n):
+            lrs.append(sch.get_last_lr()[0])
+            opt.step()
+            sch.step()
+        out[f"lr_sched_{tag}"] = np.array(lrs, dtype=np.float64)
+
+
+def _reference_train_util():
+    """train_util.py imports heavy optional packages at module level; load only the scheduler class
+    source out of it (the class body is executed in a namespace with math + torch)."""
+    import ast
+    import math
+    src = open(os.path.join(H.REF, "comet", "models", "train_util.py")).read()
+    tree = ast.parse(src)
+    node = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "WarmupCosineRestarts")
+    ns = {"math": math, "torch": torch}
+    exec(compile(ast.Module(body=[node], type_ignores=[]), "train_util.py", "exec"), ns)
+    return types_ns(WarmupCosineRestarts=ns["WarmupCosineRestarts"])
+
+
+def types_ns(**kw):
+    import types
+    return types.SimpleNamespace(**kw)
+
+
+CFG_HEAD = dict(B=1, T=16, H=512, W=512, N=512)
+
+
+def gen_headline(out):
+    """Headline workload (BASELINE configs[1]/[2] per sequence: T=16, 512^2, N=512), B=1 (the
+    reference cannot run B>1), PRNG weights seed 0, inputs seed 1 (tests/golden/comet_golden_headline.npz).
+    Stage tensors are stored so the GPU test can pin each stage on the reference's own inputs
+    (the refine step floors coarse tracks: an fp32 ulp near an integer picks another patch):
+      coarse tracks -> (refine_track) refined tracks, raw + inverted score -> (camera_predictor)
+      pose enc, loss, gradients; plus the bf16-autocast end-to-end pose enc / loss."""
+    E2E = H.reference_module("E2Epose2")
+    cap = {}
+    orig = E2E.refine_track
+
+    def wrapped(images, fnet, fpred, coarse, **k):
+        r = orig(images, fnet, fpred, coarse, **k)
+        cap["coarse"] = coarse.detach().clone()
+        cap["refined"], cap["score"] = r[0].detach().clone(), r[1].detach().clone()
+        return r
+    E2E.refine_track = wrapped
+    try:
+        torch.manual_seed(0)
+        cfg = H.load_cfg()
+        model = H.build_reference_comet(cfg)
+        P, P_hf = reference_state(model, SEED_W)
+        model.load_state_dict(P_hf, strict=True)
+        del P, P_hf
+        QC = H.reference_module("train_eval_func_new_cp5").QuaternionCameras
+        q = CFG_HEAD
+        img, tracks, gt = prng.synthetic_batch(SEED_X, q["B"], q["T"], q["H"], q["W"], q["N"])
+        cams = QC(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+                  principal_point=gt["principal_point"], ratio=gt["ratio"])
+        vis = torch.ones(q["B"], q["T"], q["N"], dtype=torch.bool)
+        import time
+        t0 = time.time()
+        pred = model(img, gt_cameras=cams, training=True, tracks=tracks, tracks_visibility=vis)
+        model.zero_grad()
+        pred["loss"].mean().backward()
+        print(f"reference fp32 train step at headline size: {time.time() - t0:.1f} s")
+        grads = {k: p.grad for k, p in model.camera_predictor.named_parameters() if p.grad is not None}
+        names = sorted(grads)
+        inv = 1.0 / (cap["score"] + 1e-6)
+        out["head_cfg"] = np.array([SEED_W, SEED_X, q["B"], q["T"], q["H"], q["W"], q["N"]])
+        out["head_coarse"] = np32(cap["coarse"])
+        out["head_refined"] = np32(cap["refined"])
+        out["head_score"] = np32(cap["score"])
+        out["head_pred_score"] = np32(inv / inv.max(dim=1, keepdim=True)[0])
+        out["head_pred_pose_enc"] = np32(pred["pred_pose_enc"])
+        out["head_gt_pose_enc"] = np32(pred["gt_pose_enc"])
+        out["head_loss"] = np32(pred["loss"].reshape(1))
+        out["head_loss_trans"] = np32(pred["loss_trans"].reshape(1))
+        out["head_loss_rot"] = np32(pred["loss_rot"].reshape(1))
+        out["head_pred_T"] = pred["pred_cameras"].T.detach().double().numpy()
+        out["head_grad_names"] = np.array(names)
+        out["head_grad_norms"] = np.array([grads[k].double().norm().item() for k in names])
+        for k in ["fc_depth.weight", "fc_translation2d.weight", "pose_branch.fc2.weight", "trunk.3.mlp.fc2.bias",
+                  "confidence_attention.0.weight", "traj_encoder.mlp.0.weight", "pose_token"]:
+            out["head_grad_full." + k] = np32(grads[k])
+        del pred, grads
+        model.zero_grad(set_to_none=True)
+        t0 = time.time()
+        with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16):
+            pb = model(img, gt_cameras=cams, training=True, tracks=tracks, tracks_visibility=vis)
+        print(f"reference bf16 forward at headline size: {time.time() - t0:.1f} s")
+        out["head_bf16_pred_pose_enc"] = np32(pb["pred_pose_enc"].float())
+        out["head_bf16_loss"] = np32(pb["loss"].float().reshape(1))
+        out["head_bf16_refined"] = np32(pb["pred_tracks"].float())
+    finally:
+        E2E.refine_track = orig
+
+
+def main_headline():
+    H.require_reference()
+    torch.set_num_threads(8)
+    out = {}
+    gen_headline(out)
+    path = os.path.join(OUT, "comet_golden_headline.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
+def main_v2():
+    H.require_reference()
+    torch.set_num_threads(8)
+    out = {}
+    gen_v2(out)
+    path = os.path.join(OUT, "comet_golden_v2.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
 def main():
     H.require_reference()
     os.makedirs(OUT, exist_ok=True)
@@ -223,4 +432,9 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--v2" in sys.argv:
+        main_v2()
+    elif "--headline" in sys.argv:
+        main_headline()
+    else:
+        main()
