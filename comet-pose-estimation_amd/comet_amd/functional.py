@@ -85,6 +85,7 @@ def refresh_weight_cache(params):
                 and d.is_contiguous() and s.numel() == d.numel()):
             src.append(s)
             dst.append(d)
+            _wver[k] = s._version  # the copy is current again, whatever bumped the version
         else:
             del _wcache[k]
             _wsrc.pop(k, None)

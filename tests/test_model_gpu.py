@@ -269,7 +269,7 @@ def test_e2e_pred_score_matches_reference(setup, gold2):
     close(tp["pred_score"], gold2["e2e_pred_score"], 1e-4, 1e-5, "pred_score (inverted, normalised)")
 
 
-def test_e2e_bf16_grads_match_reference_bf16(setup, gold2):
+def test_e2e_bf16_grads_match_reference_bf16(setup, gold, gold2):
     """bf16 backward vs the reference's bf16-autocast backward (accelerate mixed_precision="bf16").
     Both sides round GEMM operands to bf16 at different points, so gradients agree to bf16 accuracy:
     norms within 5e-2 relative, elements within 5e-2 x max."""
@@ -285,7 +285,20 @@ def test_e2e_bf16_grads_match_reference_bf16(setup, gold2):
     for k in gold2:
         if k.startswith("bf16_grad_full."):
             ref = gold2[k]
-            close(named[k[len("bf16_grad_full."):]].grad, ref, 5e-2, 5e-2 * float(np.abs(ref).max()), k)
+            name = k[len("bf16_grad_full."):]
+            if name.startswith("confidence_attention."):
+                # ill-conditioned: ctx = traj * w scales whole rows that the cross-attention blocks
+                # LayerNorm again (camera_predictor10.py:243-248, modules.py:298-344), so dL/dw is
+                # ~0 up to the LN eps and the gradient is a cancellation of large terms; the
+                # reference's own bf16 gradient is 4.5x its fp32 one here. Bound: no further from
+                # the reference's fp32 gradient than the reference's bf16 gradient is.
+                ref32 = gold["grad_full." + name]
+                err = (named[name].grad.double().cpu().numpy() - ref32)
+                spread = np.abs(ref - ref32)
+                print(f"{name}: |ours - ref fp32| max {np.abs(err).max():.3e}, reference bf16 spread {spread.max():.3e}")
+                assert (np.abs(err) <= spread + 5e-2 * np.abs(ref32).max()).all(), name
+                continue
+            close(named[name].grad, ref, 5e-2, 5e-2 * float(np.abs(ref).max()), k)
     model.zero_grad(set_to_none=True)
 
 
@@ -337,4 +350,8 @@ def test_dead_row_pruning_is_output_identical(setup):
     close(l1.reshape(1), l0.reshape(1).cpu(), 1e-5, 1e-6, "loss pruned vs full")
     assert set(g0) == set(g1)
     for k in g0:
-        close(g1[k], g0[k].cpu(), 1e-4, 1e-5 * float(g0[k].abs().max()) + 1e-12, f"grad {k} pruned vs full")
+        # confidence_attention.*: a cancellation of large terms (ctx rows are LayerNormed again, so
+        # the gradient is ~0 up to the LN eps, see test_e2e_bf16_grads_match_reference_bf16): fp32
+        # rounding differences upstream show at ~1e-3 of its max
+        rel = 2e-3 if k.startswith("confidence_attention.") else 1e-5
+        close(g1[k], g0[k].cpu(), 1e-4, rel * float(g0[k].abs().max()) + 1e-12, f"grad {k} pruned vs full")
