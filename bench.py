@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--fwd-only", action="store_true",
                     help="BASELINE configs[1]: full COMET forward only (eval, no_grad), no loss backward / optimizer")
     ap.add_argument("--cpu-baseline-only", action="store_true")
+    ap.add_argument("--cpu-baseline-full", action="store_true",
+                    help="with --cpu-baseline-only: every SURVEY 8(d) mode (train/eval x fp32/bf16), 2 reps each")
     return ap.parse_args()
 
 
@@ -59,16 +61,37 @@ def synthetic(B, T, S_img, N, device, seed):
     return img, tracks, cams
 
 
-def cpu_baseline(T, S_img, N):
-    """The oracle (CPU fp32 restatement of the reference path) timed on this host: one
-    sequence (B=1), full train step fwd + bwd + clip + AdamW. Bounded sample ~10-40 s."""
-    from oracle import comet_oracle as O
-    from comet_amd.config import instantiate, load_config
+CPU_MODES = {
+    "train_fp32": "train step fwd+bwd+clip+AdamW, fp32",
+    "train_bf16": "train step fwd+bwd+clip+AdamW, bf16 autocast",
+    "eval_fp32": "eval forward (no_grad), fp32",
+    "eval_bf16": "eval forward (no_grad), bf16 autocast",
+}
+
+
+def cpu_host():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads():
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     if threads <= 0:
         threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    print(f"[bench] cpu baseline: oracle train step on {threads} threads ...", file=sys.stderr, flush=True)
+    return threads
+
+
+def oracle_timer(T, S_img, N):
+    """-> run(mode): one B=1 sequence through the oracle (CPU fp32 restatement of the reference
+    path, parity-pinned to it in tests/test_oracle_golden.py), SURVEY 8(d) synthetic inputs."""
+    from oracle import comet_oracle as O
+    from comet_amd.config import instantiate, load_config
     cfg = load_config()
     torch.manual_seed(0)
     m = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg)
@@ -83,21 +106,45 @@ def cpu_baseline(T, S_img, N):
     gt = {"R": torch.where(q[:, :1] < 0, -q, q), "T_uvz": torch.stack([300 + torch.rand(T) * 20, 240 + torch.rand(T) * 20,
                                                                        5 + torch.rand(T) * 10], -1),
           "T": torch.randn(T, 3), "focal_length": torch.full((T, 2), 268.44), "ratio": torch.tensor([0.5], dtype=torch.float64)}
-    t0 = time.perf_counter()
-    O.train_step(names, P, img, tracks, gt)
-    dt = time.perf_counter() - t0
-    cpu = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return {"value": 1.0 / dt, "unit": "sequences/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"1 sequence (B=1, T={T}, {S_img}x{S_img}, N={N}) train step fwd+bwd+clip+AdamW, fp32, "
-                      f"oracle/comet_oracle.py, {dt:.1f} s, host '{cpu}'"}
+
+    def run(mode):
+        kind, prec = mode.split("_")
+        ctx = torch.autocast("cpu", dtype=torch.bfloat16) if prec == "bf16" else torch.autocast("cpu", enabled=False)
+        t0 = time.perf_counter()
+        with ctx:
+            if kind == "train":
+                O.train_step(names, P, img, tracks, gt)
+            else:
+                with torch.no_grad():
+                    O.comet_forward(P, img, tracks, gt)
+        return time.perf_counter() - t0
+    return run
+
+
+def cpu_baseline(T, S_img, N, modes=("train_fp32",), reps=1, warmup_frames=4):
+    """The oracle timed on this host's cores: per mode one warm-up (a T=`warmup_frames`
+    sequence: thread pool, allocator and first-call costs, bounded) then `reps` timed sequences at
+    the full size; value = 1 / mean seconds. The default bench line is the bounded headline sample
+    (train fp32, 1 rep, ~20 s); `--cpu-baseline-full` runs every mode with 2 reps."""
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    print(f"[bench] cpu baseline: oracle {list(modes)} on {threads} threads ...", file=sys.stderr, flush=True)
+    warm = oracle_timer(warmup_frames, S_img, N)
+    run = oracle_timer(T, S_img, N)
+    res = {}
+    for mode in modes:
+        warm(mode)
+        ts = [run(mode) for _ in range(reps)]
+        res[mode] = {"s_per_seq": [round(t, 2) for t in ts], "value": len(ts) / sum(ts)}
+    main_mode = modes[0]
+    cpu = cpu_host()
+    out = {"value": res[main_mode]["value"], "unit": "sequences/s", "cores": torch.get_num_threads(), "kind": "port",
+           "sample": f"B=1 sequence (T={T}, {S_img}x{S_img}, N={N}) {CPU_MODES[main_mode]}, oracle/comet_oracle.py, "
+                     f"1 warm-up (T={warmup_frames}) + {reps} timed, {sum(res[main_mode]['s_per_seq']) / reps:.1f} s/seq, "
+                     f"host '{cpu}'"}
+    if len(modes) > 1:
+        out["modes"] = res
+    return out
 
 
 def pmc_traffic(instance, config):
@@ -123,7 +170,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.cpu_baseline_only:
-        print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks)))
+        if args.cpu_baseline_full:
+            print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks, modes=tuple(CPU_MODES), reps=2)))
+        else:
+            print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks)))
         return
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

@@ -1,0 +1,81 @@
+"""Calibration record of the CPU baseline, build container only: the REFERENCE and
+the oracle (oracle/comet_oracle.py, the object bench.py's cpu_baseline times on the GPU box) timed
+side by side on the same cores, B=1 sequence at T=16, 512^2, N=512, per mode 1 warm-up + 2 reps.
+
+    PYTHONDONTWRITEBYTECODE=1 python tools/cpu_calibrate.py > profiles/r02_cpu_calibration.json
+
+Refuses to run without /root/reference (tools/ref_harness.py)."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [ROOT, HERE, os.path.join(ROOT, "comet-pose-estimation_amd")]
+
+import ref_harness as H  # noqa: E402
+import bench  # noqa: E402
+from oracle import prng  # noqa: E402
+
+MODES = ("train_fp32", "train_bf16", "eval_fp32")
+PROBE_S = {"train_fp32": 19.2, "train_bf16": 12.3, "eval_fp32": 14.6}  # SURVEY 6 / 8(d) probes, 8 cores
+
+
+def reference_timer(T, S, N):
+    import gen_golden as G
+    torch.manual_seed(0)
+    cfg = H.load_cfg()
+    model = H.build_reference_comet(cfg)
+    P, P_hf = G.reference_state(model, 0)
+    model.load_state_dict(P_hf, strict=True)
+    del P, P_hf
+    QC = H.reference_module("train_eval_func_new_cp5").QuaternionCameras
+    img, tracks, gt = prng.synthetic_batch(1, 1, T, S, S, N)
+    cams = QC(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+              principal_point=gt["principal_point"], ratio=gt["ratio"])
+    vis = torch.ones(1, T, N, dtype=torch.bool)
+
+    def run(mode):
+        kind, prec = mode.split("_")
+        ctx = torch.autocast("cpu", dtype=torch.bfloat16) if prec == "bf16" else torch.autocast("cpu", enabled=False)
+        t0 = time.perf_counter()
+        with ctx:
+            if kind == "train":
+                pred = model(img, gt_cameras=cams, training=True, tracks=tracks, tracks_visibility=vis)
+                model.zero_grad(set_to_none=True)
+                pred["loss"].mean().backward()
+            else:
+                with torch.no_grad():
+                    model(img, gt_cameras=cams, training=False, tracks=tracks, tracks_visibility=vis)
+        return time.perf_counter() - t0
+    return run
+
+
+def main():
+    H.require_reference()
+    threads = int(os.environ.get("THREADS", "8"))
+    torch.set_num_threads(threads)
+    T, S, N = 16, 512, 512
+    rec = {"threads": threads, "host": bench.cpu_host(), "workload": f"B=1, T={T}, {S}x{S}, N={N}",
+           "method": "per mode: 1 warm-up at T=4 then 2 timed reps at the full size", "modes": {}}
+    for who, mk in (("reference", reference_timer), ("oracle", bench.oracle_timer)):
+        warm, run = mk(4, S, N), mk(T, S, N)
+        for mode in MODES:
+            warm(mode)
+            ts = [run(mode) for _ in range(2)]
+            rec["modes"].setdefault(mode, {})[who] = [round(t, 2) for t in ts]
+            print(f"{who} {mode}: {ts}", file=sys.stderr, flush=True)
+        del warm, run
+    for mode, d in rec["modes"].items():
+        r, o = sum(d["reference"]) / 2, sum(d["oracle"]) / 2
+        d["oracle_over_reference"] = round(o / r, 3)
+        d["survey_probe_s"] = PROBE_S[mode]
+        d["reference_over_probe"] = round(r / PROBE_S[mode], 3)
+    print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
