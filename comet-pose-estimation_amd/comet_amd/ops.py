@@ -94,7 +94,7 @@ def gemm_raw(a, b, c, *, m, n, k, layout_a, lda, layout_b, ldb, ldc, batch=(1, 1
     e0 = PROF.start()
     L.check(lib.comet_gemm(ctypes.byref(g), stream()), "comet_gemm")
     if e0 is not None:
-        name = "comet_gemm|" + _plan_name(layout_a, layout_b, cdt, c.dtype, ws_bytes.value > 0)
+        name = "comet_gemm|" + _plan_name(layout_a, layout_b, cdt, c.dtype, ws_bytes.value > 0 and _PLAN[0] != 3)
         if PROF.detail:
             name = (f"gemm L{layout_a}{layout_b} {a.dtype}->{c.dtype} M{m} N{n} K{k} b{batch[0]}x{batch[1]}"
                     f" act{act}{' bias' if bias is not None else ''}{' res' if resid is not None else ''}")
@@ -119,6 +119,8 @@ def _plan_name(la, lb, cdt, odt, split):
         return f"big{bn}.L{la}{lb}.{out}"
     if kind == 3:  # persistent tile kernel: _PLAN[2] = tile rows
         return f"pp{_PLAN[2]}x{bn}.L{la}{lb}.{out}"
+    if kind == 4:  # two workgroups per CU (gemm_w2.hip): _PLAN[2] = tile rows
+        return f"w2_{_PLAN[2]}x{bn}.L{la}{lb}.{out}"
     return f"tile128.L{la}{lb}.{'bf16' if cdt == torch.bfloat16 else 'f32'}.{out}"
 
 

@@ -28,6 +28,9 @@
 
 namespace comet {
 
+bool w2_ok(const comet_gemm_args& a);                      // gemm_w2.hip (opt-in: COMET_GEMM_W2)
+int launch_w2_any(const comet_gemm_args& a, hipStream_t s);  // gemm_w2.hip
+
 namespace {
 
 constexpr int BM = 128, BN = 128, NT = 256;
@@ -993,8 +996,11 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   constexpr int NMF = MI * NI;      // MFMAs per k-step
   constexpr int NRD = MI + NI;      // fragment reads per k-step
   // f32 outputs park each 8-row half block in LDS and store whole 128-B lines (the direct
-  // 4-column f32 stores ran at half speed); bf16 outputs store straight from the accumulators
-  constexpr bool PARK = std::is_same<TC, float>::value;
+  // 4-column f32 stores ran at half speed); so do bf16 outputs without an activation when the wave
+  // tile is 64 wide (tools/gpu/kscan.sh: the direct 4-column stores of 16 rows per instruction
+  // cost ~3-4 us per 256 x 256 tile, 10-18 % of a K = 384-768 GEMM). With GELU the parked path
+  // serialises the activation behind the LDS round trips (+27 %): those keep the direct stores.
+  constexpr bool PARK = std::is_same<TC, float>::value || (WCOLS % 64 == 0 && ACT == COMET_ACT_NONE);
   // parked f32 row pitch: 64-wide slabs XOR-swizzle their 16-B chunks (c ^ pswz(r): the 8 rows
   // one ds_write_b128 lane group writes hit 8 distinct chunks and the 4 (row, 4-chunk) quads of
   // each ds_read_b128 lane group of the re-read are disjoint); 96-wide slabs pad rows to 100
@@ -1412,7 +1418,8 @@ int big_bn(const comet_gemm_args& a) {
 }
 
 struct Plan {
-  int kind;      // 0 skinny, 1 256-row tile, 2 128 x 128 tile, 3 persistent tile kernel
+  int kind;      // 0 skinny, 1 256-row tile, 2 128 x 128 tile, 3 persistent tile kernel,
+                 // 4 two-workgroups-per-CU 256 x 128 kernel (gemm_w2.hip, opt-in)
   int bn;        // kind 1, 3: column tile
   int splits;    // requested K splits (before the workspace check)
   int bm = 0;    // kind 3: row tile
@@ -1491,6 +1498,7 @@ int choose_splits(const comet_gemm_args& a) {
 
 Plan make_plan(const comet_gemm_args& a) {
   if (skinny_ok(a)) return Plan{0, 0, 1};
+  if (w2_ok(a)) return Plan{4, 128, 1, 256};
   if (pp_ok(a)) {
     int tbm, tbn;
     pp_tile(a, tbm, tbn);
@@ -1873,7 +1881,7 @@ extern "C" int comet_gemm_plan(const comet_gemm_args* args, int64_t* bytes, int3
   *bytes = plan_workspace(*args, p);
   plan[0] = p.kind;
   plan[1] = p.bn;
-  plan[2] = p.kind == 3 ? p.bm : p.splits;
+  plan[2] = (p.kind == 3 || p.kind == 4) ? p.bm : p.splits;
   return COMET_OK;
 }
 
@@ -1888,6 +1896,7 @@ extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   const Plan plan = make_plan(a);
   if (plan.kind == 0) return a.dtype_c == COMET_BF16 ? launch_skinny<__bf16>(a, s) : launch_skinny<float>(a, s);
   if (plan.kind == 3) return a.dtype_c == COMET_BF16 ? launch_pp<__bf16>(a, s) : launch_pp<float>(a, s);
+  if (plan.kind == 4) return launch_w2_any(a, s);
   if (plan.kind == 1 && plan.tail && a.workspace != nullptr && a.workspace_bytes >= plan_workspace(a, plan)) {
     // slot 0: the K % 64 remainder (128 x 128 kernel, plain f32 output); slots 1..: the 256-row
     // kernel's split partials over the 64-multiple part; one reduce applies the epilogue

@@ -57,16 +57,19 @@ def main():
         b = torch.rand(N, device=dev)
         r = torch.rand(M, N, device=dev, dtype=odt) if res else None
         out = torch.empty(M, N, device=dev, dtype=odt)
+        os.environ["COMET_GEMM_NO_SK"] = "1"
+        t_pp = bench(lambda: ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt))
         os.environ["COMET_GEMM_NO_PP"] = "1"
         t_old = bench(lambda: ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt))
         ref_out = out.clone()
         del os.environ["COMET_GEMM_NO_PP"]
+        del os.environ["COMET_GEMM_NO_SK"]
         t = bench(lambda: ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt))
         err = (out.float() - ref_out.float()).abs().max().item()
         tt = bench(lambda: torch.matmul(x, w.t()))
         fl = 2.0 * M * N * K
         print(f"{M:6d} {N:5d} {K:5d} {act:3d} {str(odt)[6:]:>4} {int(res):3d} | {t:8.3f} {fl / t / 1e9:6.0f} | "
-              f"{tt:8.3f} {fl / tt / 1e9:5.0f} | {tt / t:5.2f} | no-pp {fl / t_old / 1e9:6.0f} TF/s, "
+              f"{tt:8.3f} {fl / tt / 1e9:5.0f} | {tt / t:5.2f} | no-SK {fl / t_pp / 1e9:6.0f} | 256-row {fl / t_old / 1e9:6.0f} TF/s, "
               f"max|new-old| {err:.2e}", flush=True)
 
 

@@ -1,6 +1,6 @@
 """Run one comet_gemm shape repeatedly (for rocprofv3 counter passes on a single kernel).
 
-    python tools/gemm_one.py M N K [act] [f32|bf16] [resid] [iters]
+    python tools/gemm_one.py M N K [act] [f32|bf16] [resid] [iters] [nobias]
 """
 import os
 import sys
@@ -20,7 +20,7 @@ def main():
     iters = int(sys.argv[7]) if len(sys.argv) > 7 else 20
     x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
-    b = torch.rand(N, device="cuda")
+    b = None if len(sys.argv) > 8 and sys.argv[8] == "nobias" else torch.rand(N, device="cuda")
     r = torch.rand(M, N, device="cuda", dtype=odt) if res else None
     out = torch.empty(M, N, device="cuda", dtype=odt)
     for _ in range(3):
