@@ -115,6 +115,8 @@ SIGNATURES = {
     "comet_rowscale_bwd": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp]),
     "comet_sincos_table": (_INT, [c_vp, c_vp, c_i64, _INT, c_i64, c_i64, c_vp]),
     "comet_harmonic_fwd": (_INT, [c_vp, c_vp, c_vp, c_vp, c_i64, _INT, _INT, _INT, c_vp]),
+    "comet_pose_pair_errors": (_INT, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp]),
+    "comet_pose_frame_errors": (_INT, [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp]),
     "comet_harmonic_bwd": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, _INT, _INT, c_vp]),
     "comet_pose_encode": (_INT, [c_vp, c_vp, c_vp, ctypes.c_double, c_vp, c_vp, c_i64, _INT, c_vp]),
     "comet_pose_decode": (_INT, [c_vp, c_vp, c_vp, ctypes.c_double, c_vp, ctypes.c_double, ctypes.c_double,

@@ -154,3 +154,18 @@ def train_step(model, images, gt_cameras, tracks, optimizer, lr_scheduler, cfg, 
     optimizer.step(max_norm=clip if clip and clip > 0 else None)
     lr_scheduler.step()
     return loss.detach(), preds
+
+
+def eval_step(model, images, gt_cameras, tracks, batch_size=None):
+    """One evaluation step (train_eval_func_new_cp5.py:619-671, the test_fn branch abl_ours.py
+    drives): model(..., training=False) under no_grad, loss.mean(), then the eval block's pose
+    metrics (comet_amd.metrics.pose_metrics: R_avg, T_avg, Racc / Tacc, Auc_30/10/5/3, ...)
+    added to the prediction dict."""
+    from .metrics import pose_metrics
+    with torch.no_grad():
+        preds = model(images, gt_cameras=gt_cameras, training=False, tracks=tracks)
+        loss = preds["loss"]
+        preds["loss"] = loss.mean() if torch.is_tensor(loss) else loss
+        if "gt_pose_enc" in preds and preds["gt_pose_enc"] is not None:
+            preds.update(pose_metrics(preds, gt_cameras, batch_size or images.shape[0]))
+    return preds

@@ -454,7 +454,7 @@ attn_fwd_v2_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int
                    float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2, Inner in) {
   static_assert(D == 64 || D == 96, "v2 forward: D = 64 or 96");
   constexpr int NQC = D / 32, DT = D / 16;
-  constexpr int ROWB = 2 * D, NCH = ROWB / 16;    // bytes / 16-B chunks per key row
+  constexpr int ROWB = 2 * D;                      // bytes per key row
   constexpr int TE = 64 * D;                       // bf16 elements of one K (or V) tile
   constexpr int NS = D == 64 ? 4 : 3;              // LDS ring stages (<= 80 KiB: 2 workgroups / CU)
   constexpr int PW = D / 32;                       // 1-KiB DMA pieces per wave per matrix and tile

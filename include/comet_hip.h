@@ -354,6 +354,23 @@ int comet_track_score(int dtype_feat, const float* qfeat, const void* pfeat, con
 int comet_dino_prep(int dtype_out, const float* images, void* cols, int64_t BS, int H, int W, int R,
                     int patch, int64_t ldc, const float* mean3, const float* std3, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Evaluation metrics (comet/models/metric.py; called by the eval block of
+ * train_eval_func_new_cp5.py:633-671). f32, one thread per pair / frame.
+ * comet_pose_pair_errors: camera_to_rel_deg3's all-pairs part (metric.py:214-245): world-to-view
+ *   matrices [batch*frames, 4, 4] (PyTorch3D layout [[R, 0], [T, 1]], get_matrix()), pairs i < j of
+ *   each sequence in torch.combinations order -> rotation_angle / translation_angle in degrees,
+ *   [batch * frames*(frames-1)/2] each (metric.py:561-570, 611-701).
+ * comet_pose_frame_errors: camera_to_rel_deg2 (the definition bound last, metric.py:391-451) per
+ *   frame: translation_angle(gt[:, :3], pred[:, :3]) in degrees, geodesic angle of Rp·Rgᵀ in radians
+ *   (metric.py:326-347) and the Euler angles of Rp·Rgᵀ [n, 3] (metric.py:302-323), from pose
+ *   encodings pred [n, ld_pred >= 7] (u, v, d, qw, qx, qy, qz) and gt [n, ld_gt >= 7].
+ * ------------------------------------------------------------------------------------- */
+int comet_pose_pair_errors(const float* pred_w2v, const float* gt_w2v, int64_t batch, int64_t frames,
+                           float* rot_deg, float* trans_deg, void* stream);
+int comet_pose_frame_errors(const float* pred_enc, int64_t ld_pred, const float* gt_enc, int64_t ld_gt,
+                            int64_t n, float* trans_deg, float* geo_rad, float* euler, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -650,3 +650,76 @@ def train_step(P_train, P_all, image, tracks, gt, lr=1e-5, state=None, max_norm=
         p.grad = g * coef
     opt.step()
     return loss.detach(), dict(zip(names, grads)), dict(zip(names, opt_params)), total
+
+
+# ----------------------------------------------------------------------------------------
+# evaluation metrics — metric.py; f32 like the reference
+# ----------------------------------------------------------------------------------------
+
+
+def _mat2quat(m):
+    """minipytorch3d/rotation_conversions.py:104-172 (best-conditioned candidate, w >= 0)."""
+    m00, m01, m02, m10, m11, m12, m20, m21, m22 = m.reshape(-1, 9).unbind(-1)
+    a = torch.stack([1 + m00 + m11 + m22, 1 + m00 - m11 - m22, 1 - m00 + m11 - m22, 1 - m00 - m11 + m22], -1)
+    a = torch.where(a > 0, a.clamp_min(0).sqrt(), torch.zeros_like(a))
+    cand = torch.stack([
+        torch.stack([a[:, 0] ** 2, m21 - m12, m02 - m20, m10 - m01], -1),
+        torch.stack([m21 - m12, a[:, 1] ** 2, m10 + m01, m02 + m20], -1),
+        torch.stack([m02 - m20, m10 + m01, a[:, 2] ** 2, m12 + m21], -1),
+        torch.stack([m10 - m01, m20 + m02, m21 + m12, a[:, 3] ** 2], -1)], -2)
+    cand = cand / (2.0 * a[..., None].clamp_min(0.1))
+    q = cand[torch.arange(a.shape[0]), a.argmax(-1)]
+    return torch.where(q[:, :1] < 0, -q, q)
+
+
+def _quat2mat(q):
+    r, i, j, k = q.unbind(-1)
+    two_s = 2.0 / (q * q).sum(-1)
+    return torch.stack([1 - two_s * (j * j + k * k), two_s * (i * j - k * r), two_s * (i * k + j * r),
+                        two_s * (i * j + k * r), 1 - two_s * (i * i + k * k), two_s * (j * k - i * r),
+                        two_s * (i * k - j * r), two_s * (j * k + i * r), 1 - two_s * (i * i + j * j)],
+                       -1).reshape(q.shape[:-1] + (3, 3))
+
+
+def translation_angle(tg, tp):
+    """metric.py:675-701 (ambiguity folded), degrees."""
+    tp = tp / (tp.norm(dim=1, keepdim=True) + 1e-15)
+    tg = tg / (tg.norm(dim=1, keepdim=True) + 1e-15)
+    loss = torch.clamp_min(1.0 - (tp * tg).sum(1) ** 2, 1e-15)
+    err = torch.acos(torch.sqrt(1 - loss))
+    err[torch.isnan(err) | torch.isinf(err)] = 1e6
+    deg = err * 180.0 / math.pi
+    return torch.min(deg, (180 - deg).abs())
+
+
+def pose_pair_errors(pred_w2v, gt_w2v, B):
+    """metric.py:214-245 (batched_all_pairs 561-570, closed_form_inverse 611-642, rotation_angle
+    645-659) -> (rel_rangle_deg, rel_tangle_deg)."""
+    S = gt_w2v.shape[0] // B
+    i1_, i2_ = torch.combinations(torch.arange(S), 2).unbind(-1)
+    i1 = (i1_[None] + torch.arange(B)[:, None] * S).reshape(-1)
+    i2 = (i2_[None] + torch.arange(B)[:, None] * S).reshape(-1)
+
+    def inv(se3):
+        Rt = se3[:, :3, :3].transpose(1, 2)
+        left = torch.cat((Rt, -se3[:, 3:, :3].bmm(Rt)), 1)
+        return torch.cat((left, se3[:, :, 3:]), -1)
+    rg = inv(gt_w2v[i1]).bmm(gt_w2v[i2])
+    rp = inv(pred_w2v[i1]).bmm(pred_w2v[i2])
+    qg, qp = _mat2quat(rg[:, :3, :3]), _mat2quat(rp[:, :3, :3])
+    loss = (1 - (qp * qg).sum(1) ** 2).clamp(min=1e-15)
+    return torch.arccos(1 - 2 * loss) * 180 / math.pi, translation_angle(rg[:, 3, :3], rp[:, 3, :3])
+
+
+def pose_frame_errors(pred_enc, gt_enc):
+    """metric.py:391-451 core -> (translation angle deg, geodesic rad, Euler [n, 3] rad float64)."""
+    tr = translation_angle(gt_enc[:, :3], pred_enc[:, :3])
+    m = torch.bmm(_quat2mat(pred_enc[:, 3:7]), _quat2mat(gt_enc[:, 3:7]).transpose(1, 2))
+    cos = ((m[:, 0, 0] + m[:, 1, 1] + m[:, 2, 2] - 1) / 2).clamp(-1, 1)
+    md = m.double()
+    sy = torch.sqrt(md[:, 0, 0] ** 2 + md[:, 1, 0] ** 2)
+    sing = sy < 1e-6
+    z = torch.where(sing, torch.atan2(-md[:, 1, 2], md[:, 1, 1]), torch.atan2(md[:, 2, 1], md[:, 2, 2]))
+    y = torch.atan2(-md[:, 2, 0], sy)
+    x = torch.where(sing, torch.zeros_like(sy), torch.atan2(md[:, 1, 0], md[:, 0, 0]))
+    return tr, torch.acos(cos), torch.stack([x, y, z], -1)

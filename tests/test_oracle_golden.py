@@ -210,3 +210,22 @@ def test_headline_stages_match_reference(headline, full_params):
     close(out["pred_pose_enc"], g["head_pred_pose_enc"], 1e-5, 1e-5, "headline pose enc")
     close(out["loss"].reshape(1), g["head_loss"], 1e-5, 1e-6, "headline loss")
     close(out["pred_T"], g["head_pred_T"], 1e-5, 1e-4, "headline pred T")
+
+
+# ---- §8(f3) evaluation metrics: oracle vs the reference metric.py (comet_golden_metrics.npz) ----
+@pytest.fixture(scope="module")
+def gold_metrics():
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "comet_golden_metrics.npz"), allow_pickle=False))
+
+
+@pytest.mark.parametrize("tag", ["a", "b", "c"])
+def test_metrics_oracle_matches_reference(gold_metrics, tag):
+    g = {k[3:]: v for k, v in gold_metrics.items() if k.startswith(f"m{tag}_")}
+    B = int(g["cfg"][1])
+    rot, tr = O.pose_pair_errors(torch.from_numpy(g["pred_w2v"]), torch.from_numpy(g["gt_w2v"]), B)
+    close(rot, g["d3_rel_rangle"], 1e-5, 1e-3, "pair rotation error (deg)")
+    close(tr, g["d3_rel_tangle"], 1e-5, 1e-3, "pair translation error (deg)")
+    ftr, geo, eul = O.pose_frame_errors(torch.from_numpy(g["pred_enc"]), torch.from_numpy(g["gt_enc"]))
+    close(torch.rad2deg(geo), g["d2_rel_rangle"], 1e-5, 1e-3, "geodesic error (deg)")
+    close(ftr, g["d2_rel_tangle"], 1e-5, 1e-3, "frame translation error (deg)")
+    close(np.rad2deg(np.abs(eul.numpy()).mean(0)), g["d2_error_euler"], 1e-6, 1e-6, "mean |Euler| (deg)")

@@ -413,6 +413,97 @@ def main_v2():
     print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
 
 
+def _metric_case(seed, B, S):
+    """Synthetic eval outputs for the metric fixtures: world-to-view matrices [[R, 0], [T, 1]] (f32)
+    of GT and predicted cameras, absolute T, and 7/8-column pose encodings, with edge cases: exact
+    matches (zero error), a 180-degree flip, a 90-degree pitch (Euler singularity) and a zero
+    translation."""
+    from minipytorch3d import rotation_conversions as rc
+    g = torch.Generator().manual_seed(seed)
+    n = B * S
+    qg = torch.randn(n, 4, generator=g)
+    qg = qg / qg.norm(dim=-1, keepdim=True)
+    dq = torch.randn(n, 4, generator=g) * torch.rand(n, 1, generator=g) * 0.3
+    qp = qg + dq
+    qp = qp / qp.norm(dim=-1, keepdim=True)
+    qp[0] = qg[0]                                     # exact match
+    qp[3] = torch.tensor([qg[3, 1], -qg[3, 0], qg[3, 3], -qg[3, 2]])  # 180-degree relative flip
+    qp[5] = torch.tensor([0.7071068, 0.0, 0.7071068, 0.0])            # 90-degree pitch
+    Tg = torch.randn(n, 3, generator=g) * 2
+    Tp = Tg + torch.randn(n, 3, generator=g) * 0.2
+    Tp[0] = Tg[0]
+    Tp[7] = 0.0                                       # zero translation
+    def w2v(q, T):
+        M = torch.zeros(n, 4, 4)
+        M[:, :3, :3] = rc.quaternion_to_matrix(q)
+        M[:, 3, :3] = T
+        M[:, 3, 3] = 1.0
+        return M
+    enc_g = torch.cat([torch.randn(n, 3, generator=g), qg, torch.zeros(n, 1)], 1)
+    enc_p = torch.cat([enc_g[:, :3] + torch.randn(n, 3, generator=g) * 0.1, qp], 1)
+    enc_p[0] = enc_g[0, :7]
+    enc_p[2, :3] = 0.0
+    return w2v(qp, Tp), w2v(qg, Tg), Tp.double(), Tg, enc_p, enc_g
+
+
+class _Cams:
+    """The two camera attributes metric.py reads: .T and get_world_to_view_transform().get_matrix()."""
+    def __init__(self, M, T):
+        self.T, self._M = T, M
+
+    def get_world_to_view_transform(self):
+        return self
+
+    def get_matrix(self):
+        return self._M
+
+
+def gen_metrics(out):
+    """SURVEY §8(f3) fixtures (tests/golden/comet_golden_metrics.npz): the reference metric.py on
+    synthetic eval outputs -- camera_to_rel_deg3, camera_to_rel_deg2 (the binding metric.py leaves in
+    effect), calculate_auc, and the eval block of train_eval_func_new_cp5.py:633-671."""
+    H.install_stubs()
+    M = H.reference_module("metric")
+    cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self  # metric.py:337-338 hard-codes .cuda()
+    try:
+        for tag, (seed, B, S) in {"a": (11, 1, 16), "b": (12, 4, 16), "c": (13, 2, 64)}.items():
+            Mp, Mg, Tp, Tg, ep, eg = _metric_case(seed, B, S)
+            pc, gc = _Cams(Mp, Tp), _Cams(Mg, Tg)
+            r3 = M.camera_to_rel_deg3(pc, gc, "cpu", B)
+            r2 = M.camera_to_rel_deg2(ep, eg, "cpu", B)
+            auc, hist = M.calculate_auc(r3[0], r3[1], max_threshold=30, return_list=True)
+            pre = f"m{tag}_"
+            out[pre + "cfg"] = np.array([seed, B, S])
+            out[pre + "pred_w2v"], out[pre + "gt_w2v"] = np32(Mp), np32(Mg)
+            out[pre + "pred_T"], out[pre + "gt_T"] = Tp.numpy(), np32(Tg)
+            out[pre + "pred_enc"], out[pre + "gt_enc"] = np32(ep), np32(eg)
+            for k, v in zip(["rel_rangle", "rel_tangle", "T_avg", "Tx", "Ty", "Tz"], r3):
+                out[pre + "d3_" + k] = np.asarray(v.detach().double().numpy())
+            out[pre + "d2_rel_rangle"] = r2[0].double().numpy()
+            out[pre + "d2_rel_tangle"] = r2[1].double().numpy()
+            out[pre + "d2_avg"] = np.array([float(r2[2])])
+            out[pre + "d2_error_euler"] = np.asarray(r2[3], dtype=np.float64)
+            out[pre + "d2_acc5"] = np.asarray(r2[4], dtype=np.float64)
+            out[pre + "auc30"] = np.array([float(auc)])
+            out[pre + "hist"] = hist.double().numpy()
+            for th in (30, 10, 5, 3):
+                out[pre + f"auc_{th}"] = np.array([float(torch.cumsum(hist[:th], dim=0).mean())])
+            print(tag, "pairs", r3[0].numel(), "auc30", float(auc), "R_avg", float(r2[2]))
+    finally:
+        torch.Tensor.cuda = cuda
+
+
+def main_metrics():
+    H.require_reference()
+    torch.set_num_threads(8)
+    out = {}
+    gen_metrics(out)
+    path = os.path.join(OUT, "comet_golden_metrics.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
 def main():
     H.require_reference()
     os.makedirs(OUT, exist_ok=True)
@@ -434,6 +525,8 @@ def main():
 if __name__ == "__main__":
     if "--v2" in sys.argv:
         main_v2()
+    elif "--metrics" in sys.argv:
+        main_metrics()
     elif "--headline" in sys.argv:
         main_headline()
     else:
