@@ -33,6 +33,14 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class RowLNArgs(ctypes.Structure):
+    _fields_ = [
+        ("y16", c_vp), ("ldy", c_i64), ("eps_y", ctypes.c_float),
+        ("z16", c_vp), ("ldz", c_i64), ("zw", c_vp), ("zb", c_vp), ("eps_z", ctypes.c_float),
+        ("raw_c", c_i32),
+    ]
+
+
 class ConvArgs(ctypes.Structure):
     _fields_ = [
         ("dtype", c_i32), ("dtype_y", c_i32),
@@ -84,6 +92,8 @@ SIGNATURES = {
     "comet_gemm": (_INT, [ctypes.POINTER(GemmArgs), c_vp]),
     "comet_gemm_workspace": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64)]),
     "comet_gemm_plan": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_int32)]),
+    "comet_gemm_rowln_ok": (_INT, [ctypes.POINTER(GemmArgs)]),
+    "comet_gemm_rowln": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(RowLNArgs), c_vp]),
     "comet_conv2d_nhwc": (_INT, [ctypes.POINTER(ConvArgs), c_vp]),
     "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
                                    c_i64, _F, _INT, c_vp]),

@@ -58,6 +58,75 @@ class AttnBlock(nn.Module):
         return self.mlp(F.layer_norm(x, eps=1e-6, out_dtype=F.compute_dtype()), resid=x)
 
 
+def _res_ln(x, w, b, resid, raw=True, y16_eps=None, z=None):
+    """No-grad residual Linear whose consumers are LayerNorms: (c, y16, z16) as ops.linear_rowln
+    (one kernel with the LayerNorms in its epilogue when eligible; otherwise the GEMM and the
+    LayerNorm kernels separately, same outputs). y16 / z16 are in the compute dtype."""
+    wc = F.wcast(w)
+    xc = x if x.dtype == wc.dtype else ops.cast(x, wc.dtype)
+    if ops.linear_rowln_ok(xc, wc, resid):
+        return ops.linear_rowln(xc, wc, b, resid, raw=raw, y16_eps=y16_eps, z=z)
+    cdt = F.compute_dtype()
+    c = ops.linear(xc, wc, bias=b, resid=resid, out_dtype=torch.float32)
+    y16 = z16 = None
+    if z is not None:
+        z16 = ops.layernorm(c, z[0], z[1], eps=z[2], out_dtype=cdt)
+    if not raw:
+        if cdt == torch.bfloat16:
+            c, y16 = ops.layernorm(c, eps=y16_eps, out_dtype=torch.float32, dual=True)
+        else:
+            c = y16 = ops.layernorm(c, eps=y16_eps, out_dtype=torch.float32)
+    elif y16_eps is not None:
+        y16 = ops.layernorm(c, eps=y16_eps, out_dtype=cdt)
+    return c, y16, z16
+
+
+def norm1_dual(x):
+    """(f32, compute dtype) copies of the non-affine LN (eps 1e-6) that opens AttnBlock /
+    CrossAttnBlock: the f32 copy is the block's residual (modules.py:290)."""
+    return F.layer_norm_dual(x, eps=1e-6)
+
+
+DUAL = dict(raw=False, y16_eps=1e-6)  # output consumed by the next block's norm1
+
+
+def dual_ctx(cross_blk):
+    """Output consumed by a block's norm1 and by `cross_blk`'s norm_context (affine, eps 1e-5)."""
+    n = cross_blk.norm_context
+    return dict(raw=False, y16_eps=1e-6, z=(n.weight, n.bias, n.eps))
+
+
+def _mlp_pre(blk, a, o, x32, out):
+    # x = x + out_proj(o); x = x + mlp(norm2(x)): norm2 is written by the out_proj epilogue
+    h32, h16, _ = _res_ln(o, a.out_proj.weight, a.out_proj.bias, x32, raw=True, y16_eps=1e-6)
+    hid = F.linear(h16, blk.mlp.fc1.weight, blk.mlp.fc1.bias, act=L.ACT_GELU)
+    return _res_ln(hid, blk.mlp.fc2.weight, blk.mlp.fc2.bias, h32, **out)
+
+
+@torch.no_grad()
+def attn_block_pre(blk, pre, out):
+    """AttnBlock forward (no grad: the tracker) from its norm1 outputs pre = (x32, x16); the
+    output LayerNorms the consumers need are written per `out` (see _res_ln)."""
+    x32, x16 = pre
+    a = blk.attn
+    qkv = F.linear(x16, a.in_proj_weight, a.in_proj_bias)
+    o = F.attention(qkv, None, blk.heads, x32.shape[-1])
+    return _mlp_pre(blk, a, o, x32, out)
+
+
+@torch.no_grad()
+def cross_block_pre(blk, pre, ctx16, out):
+    """CrossAttnBlock forward (no grad) from norm1(x) = pre and norm_context(context) = ctx16."""
+    x32, x16 = pre
+    C = x32.shape[-1]
+    a = blk.cross_attn
+    W, b = a.in_proj_weight, a.in_proj_bias
+    q = F.linear(x16, W[:C], b[:C])
+    kv = F.linear(ctx16, W[C:], b[C:])
+    o = F.attention(q, kv, blk.heads, C)
+    return _mlp_pre(blk, a, o, x32, out)
+
+
 class CrossAttnBlock(nn.Module):
     def __init__(self, hidden_size, context_dim, num_heads=1, mlp_ratio=4.0, **kw):
         super().__init__()

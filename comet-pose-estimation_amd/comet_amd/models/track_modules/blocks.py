@@ -13,7 +13,8 @@ import torch.nn as nn
 
 from ... import functional as F
 from ... import ops
-from ..modules import AttnBlock, CrossAttnBlock, ResidualBlock, conv2d_nhwc
+from ..modules import (DUAL, AttnBlock, CrossAttnBlock, ResidualBlock, attn_block_pre, conv2d_nhwc,
+                       cross_block_pre, dual_ctx, norm1_dual)
 
 
 class BasicEncoder(nn.Module):
@@ -138,24 +139,43 @@ class EfficientUpdateFormer(nn.Module):
         B, N0, T, _ = input_tensor.shape
         C = self.hidden_size
         init = F.linear(input_tensor, self.input_transform.weight, self.input_transform.bias, out_dtype=torch.float32)
-        pts = init
+        # every block below starts with a LayerNorm of its input; except for the first ones, those
+        # LayerNorms are written by the epilogue of the GEMM that produces the input (the output
+        # specs name the consumers), so the token streams move as norm1 pairs (f32, bf16)
+        pts = norm1_dual(init.reshape(B * N0, T, C))
         vts = None
         if self.add_space_attn:
-            vts = self.virual_tracks.detach().float().expand(B, -1, T, -1).contiguous()
+            vts = norm1_dual(self.virual_tracks.detach().float().expand(B, -1, T, -1).reshape(-1, T, C).contiguous())
         Nv = self.num_virtual_tracks if self.add_space_attn else 0
         j = 0
         space_every = len(self.time_blocks) // len(self.space_virtual_blocks) if self.add_space_attn else 0
-        for i in range(len(self.time_blocks)):
+        nl = len(self.time_blocks)
+        for i in range(nl):
             blk = self.time_blocks[i]
-            pts = blk(pts.reshape(B * N0, T, C)).reshape(B, N0, T, C)
-            if vts is not None:
-                vts = blk(vts.reshape(B * Nv, T, C)).reshape(B, Nv, T, C)
-            if self.add_space_attn and i % space_every == 0:
-                vts = self.space_virtual2point_blocks[j](vts, pts)
-                vts = self.space_virtual_blocks[j](vts)
-                pts = self.space_point2virtual_blocks[j](pts, vts)
+            space = self.add_space_attn and i % space_every == 0
+            last = i == nl - 1
+            if space:
+                v2p, vself, p2v = (self.space_virtual2point_blocks[j], self.space_virtual_blocks[j],
+                                   self.space_point2virtual_blocks[j])
+                # time block on the point tracks: its output is norm1 of point<-virtual and the
+                # context of virtual<-point
+                p32, p16, pctx = attn_block_pre(blk, pts, dual_ctx(v2p))
+                v32, v16, _ = attn_block_pre(blk, vts, DUAL)
+                r4 = lambda t, n: t.reshape(B, n, T, C)
+                v32, v16, _ = cross_block_pre(v2p, (r4(v32, Nv), r4(v16, Nv)), r4(pctx, N0), DUAL)
+                v32, v16, vctx = attn_block_pre(vself, (v32, v16), dual_ctx(p2v))
+                p32, p16, _ = cross_block_pre(p2v, (r4(p32, N0), r4(p16, N0)), vctx,
+                                              dict(raw=True) if last else DUAL)
+                pts = (p32.reshape(B * N0, T, C), None if p16 is None else p16.reshape(B * N0, T, C))
+                vts = (v32.reshape(B * Nv, T, C), v16.reshape(B * Nv, T, C))
                 j += 1
-        return _flow(pts, init, self.flow_head)
+            else:
+                p32, p16, _ = attn_block_pre(blk, pts, dict(raw=True) if last else DUAL)
+                pts = (p32, p16)
+                if vts is not None:
+                    v32, v16, _ = attn_block_pre(blk, vts, DUAL)
+                    vts = (v32, v16)
+        return _flow(pts[0].reshape(B, N0, T, C), init, self.flow_head)
 
 
 def _flow(tokens, init, head):

@@ -167,6 +167,74 @@ def linear(x, w, bias=None, act=L.ACT_NONE, resid=None, out=None, out_dtype=None
     return out
 
 
+def _rowln_args(x2, wc, o2, bias, r2):
+    M, K = x2.shape
+    N = wc.shape[0]
+    g = L.GemmArgs()
+    g.dtype_ab, g.dtype_c, g.layout_a, g.layout_b = L.BF16, L.F32, 0, 0
+    g.m, g.n, g.k = M, N, K
+    g.batch[0] = g.batch[1] = 1
+    g.a, g.lda = x2.data_ptr(), x2.stride(0)
+    g.b, g.ldb = wc.data_ptr(), wc.stride(0)
+    g.c, g.ldc = o2.data_ptr(), o2.stride(0)
+    g.bias, g.bias_mode = _p(bias), (1 if bias is not None else 0)
+    g.resid, g.ldr = r2.data_ptr(), r2.stride(0)
+    g.alpha, g.beta, g.act = 1.0, 1.0, L.ACT_NONE
+    return g
+
+
+def linear_rowln_ok(x, w, resid):
+    """True when comet_gemm_rowln takes this Linear (bf16 operands, f32 residual output, N in
+    {256, 384}, K % 64 == 0, M >= 4096; see include/comet_hip.h)."""
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or resid is None or resid.dtype != torch.float32:
+        return False
+    K, N = x.shape[-1], w.shape[0]
+    if N not in (256, 384) or resid.shape[-1] != N or x.stride(-1) != 1 or w.stride(-1) != 1:
+        return False
+    x2 = x.reshape(-1, K)
+    r2 = resid.reshape(-1, N)
+    g = _rowln_args(x2, w, r2, None, r2)
+    return bool(L.load().comet_gemm_rowln_ok(ctypes.byref(g)))
+
+
+def linear_rowln(x, w, bias, resid, *, raw=True, y16_eps=None, z=None):
+    """v = x @ w^T + bias + resid (f32) with the row LayerNorms its consumers need written by the
+    same kernel (comet_gemm_rowln). Returns (c, y16, z16):
+      c   = v (raw) or LN(v; y16_eps) in f32 (raw=False: the dual copy of AttnBlock norm1),
+      y16 = LN(v; y16_eps) in bf16 when y16_eps is not None,
+      z16 = LN(v; z_eps) * z_w + z_b in bf16 when z = (z_w, z_b, z_eps)."""
+    _req_cuda(x, w, bias, resid)
+    K, N = x.shape[-1], w.shape[0]
+    x2 = x.reshape(-1, K)
+    r2 = resid.reshape(-1, N)
+    M = x2.shape[0]
+    c = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.float32)
+    o2 = c.view(-1, N)
+    g = _rowln_args(x2, w, o2, bias, r2)
+    a = L.RowLNArgs()
+    a.raw_c = 1 if raw else 0
+    y16 = z16 = None
+    if y16_eps is not None or not raw:
+        if y16_eps is None:
+            raise L.CometHipError("linear_rowln: raw=False needs y16_eps")
+        a.eps_y = float(y16_eps)
+        y16 = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.bfloat16)
+        a.y16, a.ldy = y16.data_ptr(), N
+    if z is not None:
+        zw, zb, zeps = z
+        z16 = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.bfloat16)
+        a.z16, a.ldz, a.zw, a.zb, a.eps_z = z16.data_ptr(), N, zw.data_ptr(), zb.data_ptr(), float(zeps)
+    e0 = PROF.start()
+    L.check(L.load().comet_gemm_rowln(ctypes.byref(g), ctypes.byref(a), stream()), "comet_gemm_rowln")
+    if e0 is not None:
+        name = "comet_gemm_rowln"
+        if PROF.detail:
+            name = f"gemm_rowln M{M} N{N} K{K} raw{int(raw)} y16{int(y16 is not None)} z16{int(z16 is not None)}"
+        io = 2 * M * K + 2 * K * N + 4 * M * N * 2 + 2 * M * N * ((y16 is not None) + (z16 is not None))
+        PROF.stop(e0, name, 2.0 * M * N * K, float(io))
+    return c, y16, z16
+
+
 # ------------------------------------------------------------------------------------------
 # LayerNorm
 # ------------------------------------------------------------------------------------------

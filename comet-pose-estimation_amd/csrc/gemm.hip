@@ -980,11 +980,24 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int SG_MFMA = 0x008, SG_DSR = 0x100, SG_VMR = 0x020;
 
-template <typename TC, int ACT, bool HASR, int NW, int TBM, int TBN>
+// Row LayerNorm fused into the f32 epilogue when one tile spans the whole output row (N == TBN:
+// the tracker's hidden sizes 384 / 256). With v = the epilogue value of a row (bias, residual):
+//   C   = v (raw_c) or (v - mean) * rstd(eps_y)                [f32: residual stream / dual copy]
+//   y16 = (v - mean) * rstd(eps_y)                             [bf16, optional: next GEMM operand]
+//   z16 = (v - mean) * rstd(eps_z) * zw + zb                   [bf16, optional: affine context LN]
+// Mean and variance are two-pass over the values kept in registers; the four waves of a tile row
+// exchange their partial sums through a small LDS table (two workgroup barriers per tile).
+struct RowLN {
+  __bf16* y16; int64_t ldy; float eps_y;
+  __bf16* z16; int64_t ldz; const float* zw; const float* zb; float eps_z;
+  int raw_c;
+};
+
+template <typename TC, int ACT, bool HASR, int NW, int TBM, int TBN, bool LN = false>
 __global__ void __launch_bounds__(NW * 64, 1)
 gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, int ntiles,
-               Epi epi) {
+               Epi epi, RowLN ln) {
   constexpr int WN = NW / 2;        // wave grid 2 x WN
   constexpr int WROWS = TBM / 2;    // wave tile rows (128 or 64)
   constexpr int WCOLS = TBN / WN;   // wave tile columns (64 or 96)
@@ -1008,7 +1021,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   constexpr int PPITCH = PSWZ ? WCOLS : WCOLS + 4;
   constexpr int PARK_F = PARK ? NW * 8 * PPITCH : 0;  // f32 elements of the park region
   auto pswz = [](int r) { return PSWZ ? ((r & 7) | ((r & 2) << 2)) : 0; };
-  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + 2 * PARK_F];
+  static_assert(!LN || (PARK && std::is_same<TC, float>::value), "row LN epilogue: parked f32 outputs only");
+  constexpr int STATS_F = LN ? 2 * TBM * WN : 0;  // f32 row-partial table (sum, sum of squares)
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + 2 * PARK_F + 2 * STATS_F];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / WN, wc = wid % WN;
@@ -1121,7 +1136,15 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       // VMEM ops per output kind of one epilogue: direct MI x NI, parked 2 x MI x (WCOLS / (8 * CPL))
       constexpr int PER = PARK ? 2 * MI * (WCOLS / (8 * (16 / (int)sizeof(TC)))) : MI * NI;
       constexpr int E = PER * (1 + (HASR ? 1 : 0)) + PER;  // C stores (+ resid loads) (+ aux stores)
-      if (epi.aux) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E > 63 ? 63 : E) : "memory");
+      if constexpr (LN) {
+        // C stores (+ resid loads) + one store per (row half, column pass) of each bf16 output
+        // (a lower bound of the VMEM ops issued after the LDS-DMA: bias / affine loads only add)
+        constexpr int E1 = E - PER, E2 = E1 + PER, E3 = E1 + 2 * PER;
+        const int nb = (ln.y16 != nullptr) + (ln.z16 != nullptr);
+        if (nb == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E1 > 63 ? 63 : E1) : "memory");
+        else if (nb == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E2 > 63 ? 63 : E2) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E3 > 63 ? 63 : E3) : "memory");
+      } else if (epi.aux) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E > 63 ? 63 : E) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E - PER > 63 ? 63 : E - PER) : "memory");
       pend = 0;
     } else {
@@ -1225,7 +1248,151 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
         }
       }
     };
-    if constexpr (PARK) {
+    if constexpr (LN) {
+      // row-LN epilogue (tiles_n == 1, N == TBN). Pass 1 is the parked pass of the plain f32
+      // epilogue; each lane's final values (8 lanes x NV columns of one row per wave) go back into
+      // the accumulator registers they were parked from, and the lane's row sum and sum of squares
+      // are reduced over the 8 lanes of the row, then over the WN waves of the tile row through
+      // the LDS table st (one barrier; var = E[v^2] - mean^2, clamped at 0). Pass 2 writes the
+      // outputs with the statistics read back per row (no per-row arrays in registers).
+      constexpr int CPL = 4, NTC = WCOLS / (8 * CPL), NV = NTC * CPL;
+      float* park = reinterpret_cast<float*>(smem + 2 * BUF) + wid * 8 * PPITCH;
+      float* st = reinterpret_cast<float*>(smem + 2 * BUF + 2 * PARK_F);
+      const int rr = lane >> 3, cc = lane & 7;
+      const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;  // + i*16 + h*8
+      // (tn is always 0 here; keeping it in the column makes the bias / affine loads tile-dependent
+      // so they are not hoisted out of the k-loop, where they would hold ~36 registers)
+      const int pc0 = tn * TBN + wc * WCOLS + cc * CPL;  // + t*8*CPL + e
+      const float invn = 1.f / (float)N;
+      auto VK = [&](int i, int h, int u) -> float { return acc[i][h * NTC + (u >> 2)][u & 3]; };
+      auto lrow = [&](int i, int h) { return (wr * WROWS + i * 16 + h * 8 + rr) * WN; };
+      auto red8 = [](float x) {
+        x += __shfl_xor(x, 1, 64);
+        x += __shfl_xor(x, 2, 64);
+        x += __shfl_xor(x, 4, 64);
+        return x;
+      };
+      // (mean, biased variance) of row (i, h) from the WN (sum, sum of squares) partials
+      auto rowstats = [&](int i, int h, float& mu, float& var) {
+        float x = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WN; ++w) {
+          const float2 p = *reinterpret_cast<const float2*>(st + 2 * (lrow(i, h) + w));
+          x += p.x;
+          q += p.y;
+        }
+        mu = x * invn;
+        var = fmaxf(q * invn - mu * mu, 0.f);
+      };
+      auto lnepilogue = [&](auto edge_t) {
+        constexpr bool EDGE = decltype(edge_t)::value;
+        float bcp[NV];
+#pragma unroll
+        for (int u = 0; u < NV; ++u) bcp[u] = 0.f;
+        if (epi.bias != nullptr) {
+#pragma unroll
+          for (int t = 0; t < NTC; ++t) load4(epi.bias + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(bcp + t * CPL));
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          float vh[2][NV];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int64_t row = prow0 + i * 16 + h * 8;
+            const bool live = !EDGE || row < M;
+            float rc[NTC][CPL];
+#pragma unroll
+            for (int t = 0; t < NTC; ++t)
+#pragma unroll
+              for (int e = 0; e < CPL; ++e) rc[t][e] = 0.f;
+            if constexpr (HASR) {
+#pragma unroll
+              for (int t = 0; t < NTC; ++t)
+                if (live) loadn<CPL>(R + row * epi.ldr + pc0 + t * 8 * CPL, rc[t]);
+            }
+            if ((li >> 3) == h) {
+#pragma unroll
+              for (int j = 0; j < NI; ++j)
+                *reinterpret_cast<f32x4*>(park + (li & 7) * PPITCH + (((j * 4 + g) ^ pswz(li & 7)) << 2)) = acc[i][j];
+            }
+            asm volatile("" ::: "memory");
+            float s = 0.f, sq = 0.f;
+#pragma unroll
+            for (int t = 0; t < NTC; ++t) {
+              float v[CPL];
+              const int lc = (t * 8 * CPL + cc * CPL) >> 2;
+              const f32x4 p4 = *reinterpret_cast<const f32x4*>(park + rr * PPITCH + ((lc ^ pswz(rr)) << 2));
+              v[0] = p4[0]; v[1] = p4[1]; v[2] = p4[2]; v[3] = p4[3];
+#pragma unroll
+              for (int e = 0; e < CPL; ++e) {
+                float o = apply_act(ACT, epi.alpha * v[e] + bcp[t * CPL + e]);
+                if constexpr (HASR) o += epi.beta * rc[t][e];
+                v[e] = o;
+                vh[h][t * CPL + e] = o;
+                s += o;
+                sq = fmaf(o, o, sq);
+              }
+              if (ln.raw_c && live) storen<CPL>(C + row * ldc + pc0 + t * 8 * CPL, v);
+            }
+            s = red8(s);
+            sq = red8(sq);
+            if (cc == 0) *reinterpret_cast<float2*>(st + 2 * (lrow(i, h) + wc)) = float2{s, sq};
+            asm volatile("" ::: "memory");
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int t = 0; t < NTC; ++t)
+              acc[i][h * NTC + t] = f32x4{vh[h][4 * t], vh[h][4 * t + 1], vh[h][4 * t + 2], vh[h][4 * t + 3]};
+        }
+        float zw[NV], zb[NV];
+        if (ln.z16 != nullptr) {
+#pragma unroll
+          for (int t = 0; t < NTC; ++t) {
+            load4(ln.zw + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(zw + t * CPL));
+            load4(ln.zb + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(zb + t * CPL));
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        // pass 2: outputs, row by row (mean / rstd once per row, affine weights loaded before the
+        // barrier: a load issued after this epilogue's stores would wait for them)
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int64_t row = prow0 + i * 16 + h * 8;
+            if (EDGE && row >= M) continue;
+            float mu, var;
+            rowstats(i, h, mu, var);
+            const float ry = rsqrtf(var + ln.eps_y), rz = rsqrtf(var + ln.eps_z);
+#pragma unroll
+            for (int t = 0; t < NTC; ++t) {
+              const int col = pc0 + t * 8 * CPL;
+              float y[CPL];
+#pragma unroll
+              for (int e = 0; e < CPL; ++e) y[e] = (VK(i, h, t * CPL + e) - mu) * ry;
+              if (!ln.raw_c) storen<CPL>(C + row * ldc + col, y);
+              if (ln.y16 != nullptr) store4(ln.y16 + row * ln.ldy + col, y);
+              if (ln.z16 != nullptr) {
+                float z[CPL];
+#pragma unroll
+                for (int e = 0; e < CPL; ++e)
+                  z[e] = (VK(i, h, t * CPL + e) - mu) * rz * zw[t * CPL + e] + zb[t * CPL + e];
+                store4(ln.z16 + row * ln.ldz + col, z);
+              }
+            }
+          }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      };
+      if (interior) lnepilogue(std::false_type{});
+      else lnepilogue(std::true_type{});
+      // the next tile's k-step-0 fragments again (buffer (q+1)&1 still holds k-tile q+1): the
+      // copies read during k-step 1 are dead here, so their registers serve the epilogue
+      read_frags((q + 1) & 1, 0, a0, b0);
+    } else if constexpr (PARK) {
       // parked epilogue: per 8-row half of each 16-row block the wave parks its 8 x WCOLS raw
       // accumulators in its own LDS slab (no barrier: only this wave touches it) and re-reads them
       // row-contiguously, so every store / residual load instruction covers 8 rows x 128 B
@@ -1361,9 +1528,37 @@ void pp_tile(const comet_gemm_args& a, int& tbm, int& tbn) {
   if (cdiv(a.m, tbm) * cdiv(a.n, tbn) < cus) tbm /= 2;
 }
 
+// Row-LN launch (comet_gemm_rowln): f32 output with a residual, no activation / aux, one tile
+// spanning the row. Instances: 128 x 384 / 64 x 384 (N = 384), 128 x 256 (N = 256).
+int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s) {
+  Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, a.alpha, COMET_ACT_NONE, 1};
+  int grid = num_cus();
+  grid -= grid % 8;
+  int tbm, tbn;
+  pp_tile(a, tbm, tbn);
+  // tile rows: full-height 128 x 384 only for long K (K >= 1024: fc2), else the half-height tiles
+  // (the full-height LN instances run at 256 VGPRs with spills; tools/rowln_bench.py)
+  const bool full = tbn == 384 && a.k >= 1024 && getenv("COMET_ROWLN_HALF") == nullptr;
+  if (!full && tbm == (tbn == 384 ? 128 : 256)) tbm /= 2;
+  const int64_t tiles_m = cdiv(a.m, tbm);
+  COMET_CHECK_ARG(tbn == a.n && tiles_m < (1ll << 30), "comet_gemm_rowln: the row must fit one tile");
+  const int ntiles = (int)tiles_m;
+  if (ntiles <= grid) grid = ntiles;
+#define PPLN(BMT, BNT)                                                                                         \
+  hipLaunchKernelGGL((w4::gemm_w4_kernel<float, COMET_ACT_NONE, true, 8, BMT, BNT, true>), dim3((unsigned)grid), \
+                     dim3(512), 0, s, (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (float*)a.c, a.ldc,  \
+                     a.m, a.n, a.k, 1, ntiles, e, ln)
+  if (tbn == 384) { if (tbm == 64) PPLN(64, 384); else PPLN(128, 384); }
+  else PPLN(128, 256);
+#undef PPLN
+  COMET_CHECK_LAUNCH("comet_gemm_rowln (persistent, row LN epilogue)");
+  return COMET_OK;
+}
+
 template <typename TC>
 int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
+  const w4::RowLN noln{};
   // N = 384 (the tracker's hidden size): 128 x 384 tiles (each A row block read once);
   // otherwise 256 x 256
   int grid = num_cus();
@@ -1378,7 +1573,7 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
 #define PPKT(ACT, HR, BMT, BNT)                                                                               \
   hipLaunchKernelGGL((w4::gemm_w4_kernel<TC, ACT, HR, 8, BMT, BNT>), dim3((unsigned)grid), dim3(512), 0, s,   \
                      (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, a.n, a.k,     \
-                     (int)tiles_n, ntiles, e)
+                     (int)tiles_n, ntiles, e, noln)
 #define PPK(ACT, HR)                                                                                          \
   do {                                                                                                        \
     if (n384) { if (half) PPKT(ACT, HR, 64, 384); else PPKT(ACT, HR, 128, 384); }                           \
@@ -1883,6 +2078,40 @@ extern "C" int comet_gemm_plan(const comet_gemm_args* args, int64_t* bytes, int3
   plan[1] = p.bn;
   plan[2] = (p.kind == 3 || p.kind == 4) ? p.bm : p.splits;
   return COMET_OK;
+}
+
+// Row-LN GEMM (see w4::RowLN): eligibility shared by comet_gemm_rowln_ok and comet_gemm_rowln.
+static bool rowln_ok(const comet_gemm_args& a, const comet_rowln_args* ln) {
+  using namespace comet;
+  if (!pp_ok(a) || a.dtype_c != COMET_F32 || a.resid == nullptr || a.aux != nullptr || a.act != COMET_ACT_NONE) return false;
+  if (a.n != 384 && a.n != 256) return false;
+  int tbm, tbn;
+  pp_tile(a, tbm, tbn);
+  if (tbn != a.n) return false;
+  if (ln == nullptr) return true;
+  auto b4 = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 8 == 0 && ld % 4 == 0); };
+  if (!b4(ln->y16, ln->ldy) || !b4(ln->z16, ln->ldz)) return false;
+  if (ln->z16 != nullptr && (ln->zw == nullptr || ln->zb == nullptr)) return false;
+  return true;
+}
+
+extern "C" int comet_gemm_rowln_ok(const comet_gemm_args* args) {
+  using namespace comet;
+  if (args == nullptr || validate(args) != COMET_OK) return 0;
+  return rowln_ok(*args, nullptr) ? 1 : 0;
+}
+
+extern "C" int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_args* ln, void* stream) {
+  using namespace comet;
+  const int rc = validate(args);
+  if (rc != COMET_OK) return rc;
+  COMET_CHECK_ARG(ln != nullptr && args->a && args->b && args->c, "comet_gemm_rowln: null operand");
+  COMET_CHECK_ARG(rowln_ok(*args, ln), "comet_gemm_rowln: not eligible (bf16 k-contiguous operands, K % 64 == 0, "
+                                       "M >= 4096, N in {256, 384}, f32 output with a residual, no activation / aux)");
+  if (args->m == 0) return COMET_OK;
+  w4::RowLN r{reinterpret_cast<__bf16*>(ln->y16), ln->ldy, ln->eps_y, reinterpret_cast<__bf16*>(ln->z16), ln->ldz,
+              ln->zw, ln->zb, ln->eps_z, ln->raw_c};
+  return launch_pp_rowln(*args, r, as_stream(stream));
 }
 
 extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {

@@ -89,6 +89,23 @@ int comet_gemm_workspace(const comet_gemm_args* args, int64_t* bytes);
  * Lets a profiler name the kernel instance a call lands on (bench.py roofline). */
 int comet_gemm_plan(const comet_gemm_args* args, int64_t* bytes, int32_t* plan);
 
+/* GEMM + row LayerNorm epilogue (AttnBlock / CrossAttnBlock of the tracker's update former,
+ * blocks.py:205-348 over modules.py:248-344, all under no_grad): the f32 residual GEMM whose
+ * output row v = x @ w^T + bias + beta*resid feeds LayerNorms (norm2 of the same block; norm1 /
+ * norm_context of the next blocks) writes those LayerNorms itself:
+ *   c   = v when raw_c != 0, else (v - mean(v)) / sqrt(var(v) + eps_y)        [f32]
+ *   y16 = (v - mean(v)) / sqrt(var(v) + eps_y)                                  [bf16, optional]
+ *   z16 = (v - mean(v)) / sqrt(var(v) + eps_z) * zw + zb                        [bf16, optional]
+ * (biased variance, as nn.LayerNorm). Eligible (comet_gemm_rowln_ok): bf16 k-contiguous A / B,
+ * K % 64 == 0, M >= 4096, N in {256, 384}, dtype_c f32 with resid, act NONE, no aux, no split. */
+typedef struct comet_rowln_args {
+  void* y16; int64_t ldy; float eps_y;
+  void* z16; int64_t ldz; const float* zw; const float* zb; float eps_z;
+  int32_t raw_c;
+} comet_rowln_args;
+int comet_gemm_rowln_ok(const comet_gemm_args* args);
+int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_args* ln, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM convolution on channels-last activations (nn.Conv2d of BasicEncoder /
  * ShallowEncoder / ResidualBlock, blocks.py:27-202, modules.py:39-116): the im2col matrix is

@@ -799,3 +799,55 @@ def test_cast_multi_and_weight_cache_refresh():
     assert Fn.wcast(w) is c_full and torch.equal(c_full, w.detach().to(torch.bfloat16))
     assert torch.equal(Fn.wcast(w[:128]), w.detach()[:128].to(torch.bfloat16))
     Fn.invalidate_weight_cache([w])
+
+
+@pytest.mark.parametrize("mnk", [(65536, 384, 384), (8192, 384, 1536), (8192 + 40, 384, 384), (65536, 256, 256),
+                                 (8192, 256, 1024), (4096 + 100, 256, 256)])
+@pytest.mark.parametrize("mode", ["raw_y16", "dual", "dual_ctx", "raw_only"])
+def test_gemm_rowln(mnk, mode):
+    """comet_gemm_rowln: residual GEMM with the consumers' row LayerNorms in the epilogue (tracker
+    update former, modules.py:248-344) vs f64: one tile spans the row (N = 384: 128 x 384 / 64 x 384
+    tiles; N = 256: 256 x 256 / 128 x 256), M tails take the edge copy of the epilogue."""
+    ops = _ops()
+    M, N, K = mnk
+    x = _rand(M, K, seed=101).to(torch.bfloat16)
+    w = _rand(N, K, seed=102, scale=K ** -0.5).to(torch.bfloat16)
+    b = _rand(N, seed=103, scale=0.1)
+    r = _rand(M, N, seed=104) + 0.5  # nonzero row means: the LN must remove them
+    zw, zb = _rand(N, seed=105), _rand(N, seed=106)
+    v = x.double() @ w.double().t() + b.double() + r.double()
+    mu = v.mean(-1, keepdim=True)
+    var = v.var(-1, unbiased=False, keepdim=True)
+    ln6 = (v - mu) / torch.sqrt(var + 1e-6)
+    ln5 = (v - mu) / torch.sqrt(var + 1e-5) * zw.double() + zb.double()
+    xd, wd, bd, rd = x.to(DEV), w.to(DEV), b.to(DEV), r.to(DEV)
+    assert ops.linear_rowln_ok(xd, wd, rd)
+    raw = mode in ("raw_y16", "raw_only")
+    c, y16, z16 = ops.linear_rowln(xd, wd, bd, rd, raw=raw, y16_eps=None if mode == "raw_only" else 1e-6,
+                                   z=(zw.to(DEV), zb.to(DEV), 1e-5) if mode == "dual_ctx" else None)
+    tol = 2e-5 * math.sqrt(K)
+    _close(c, v if raw else ln6, 1e-4, tol, f"rowln c {mnk} {mode}")
+    if mode == "raw_only":
+        assert y16 is None and z16 is None
+    else:
+        _close(y16, ln6, 8e-3, 8e-3, f"rowln y16 {mnk} {mode}")
+    if mode == "dual_ctx":
+        _close(z16, ln5, 8e-3, 3e-2, f"rowln z16 {mnk} {mode}")
+    torch.cuda.synchronize()
+
+
+def test_gemm_rowln_matches_separate_kernels():
+    """The fused epilogue equals the GEMM + LayerNorm kernels it replaces (bf16 outputs bit-equal
+    up to one rounding step, f32 within summation-order noise)."""
+    ops = _ops()
+    M, N, K = 16384, 384, 1536
+    x = _rand(M, K, seed=111).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=112, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
+    b = _rand(N, seed=113, scale=0.1).to(DEV)
+    r = _rand(M, N, seed=114).to(DEV)
+    c, y16, _ = ops.linear_rowln(x, w, b, r, raw=False, y16_eps=1e-6)
+    ref = ops.linear(x, w, bias=b, resid=r, out_dtype=torch.float32)
+    y32r, y16r = ops.layernorm(ref, eps=1e-6, out_dtype=torch.float32, dual=True)
+    _close(c, y32r, 1e-5, 1e-5, "rowln dual f32 vs separate")
+    d = (y16.float() - y16r.float()).abs() / y16r.float().abs().clamp_min(1e-3)
+    assert d.max().item() <= 2 ** -7, d.max().item()
