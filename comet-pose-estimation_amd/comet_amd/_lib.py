@@ -131,6 +131,8 @@ SIGNATURES = {
     "comet_pose_encode": (_INT, [c_vp, c_vp, c_vp, ctypes.c_double, c_vp, c_vp, c_i64, _INT, c_vp]),
     "comet_pose_decode": (_INT, [c_vp, c_vp, c_vp, ctypes.c_double, c_vp, ctypes.c_double, ctypes.c_double,
                                  ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_i64, _INT, c_vp]),
+    "comet_pose_encode3": (_INT, [c_vp, c_vp, c_vp, c_i64, _INT, c_vp]),
+    "comet_pose_decode3": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_vp]),
     "comet_gapr_fwd": (_INT, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, _INT, _INT, _F, _F, c_vp]),
     "comet_gapr_bwd": (_INT, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, _INT, _INT,
                               _F, _F, c_vp]),

@@ -76,6 +76,12 @@ class PoseEmbedding(nn.Module):
 
 
 class CameraPredictor(nn.Module):
+    # head variants of the ablation files (camera_predictor_abl_*.py subclass this and flip them)
+    USE_TP = True            # T_P trajectory cross-attention runs
+    TP_RESIDUAL = True       # ... and its result is added to rgb_feat (abl_track drops the add)
+    USE_TIME = True          # T_F: 1-D sincos time embedding + trunk (abl_time / abl_all drop both)
+    SINGLE_HEAD = False      # pose_branch -> 7 outputs with encoding 3 (abl_uvz / abl_all)
+
     def __init__(self, hidden_size=768, num_heads=8, mlp_ratio=4, z_dim=768, down_size=336, att_depth=4,
                  trunk_depth=4, backbone="dinov2b", pose_encoding_type="absT_quaR_OneFL", cfg=None):
         super().__init__()
@@ -95,7 +101,8 @@ class CameraPredictor(nn.Module):
                                         n_harmonic_functions=int(hidden_size / self.target_dim / 2),
                                         append_input=False)
         self.pose_token = nn.Parameter(torch.zeros(1, 1, 1, hidden_size))
-        self.pose_branch = Mlp(in_features=hidden_size, hidden_features=hidden_size * 2, out_features=4, drop=0)
+        self.pose_branch = Mlp(in_features=hidden_size, hidden_features=hidden_size * 2,
+                               out_features=7 if self.SINGLE_HEAD else 4, drop=0)
         self.ffeat_updater = nn.Sequential(nn.Linear(hidden_size, hidden_size), nn.GELU(), nn.LayerNorm(hidden_size))
         self.self_att = nn.ModuleList([AttnBlock(hidden_size, num_heads, mlp_ratio=mlp_ratio) for _ in range(att_depth)])
         self.pose_branch_scale = nn.Parameter(torch.ones(1) * 0.1)
@@ -213,7 +220,9 @@ class CameraPredictor(nn.Module):
             rgb_feat = rgb_feat_init
             B, S, C = rgb_feat.shape
         # ---- T_P ----
-        if pred_trajectories is not None:
+        # (abl_track computes T_P and discards it: nothing downstream depends on it, so it is skipped
+        # -- same outputs, and its parameters get no gradient either way)
+        if pred_trajectories is not None and self.USE_TP and self.TP_RESIDUAL:
             traj = self.traj_encoder(pred_trajectories)  # [B, S, N, C] f32
             N = traj.shape[2]
             ca = self.confidence_attention
@@ -224,14 +233,17 @@ class CameraPredictor(nn.Module):
             for blk in self.cross_attn_block:
                 r = blk(r, ctx)
             rgb_feat = F.add(rgb_feat, r.reshape(B, S, C))
+        # ---- T_F ----
+        if self.USE_TIME:
+            rgb_feat = F.add_rows(rgb_feat, self._table("1d", S, C, rgb_feat.device), S)
+            for blk in self.trunk:
+                rgb_feat = blk(rgb_feat)
+        if self.SINGLE_HEAD:
+            return self._single_head(rgb_feat, gt_cameras, B, S)
         gt_enc = None
         if gt_cameras is not None:
             gt_enc = ops.pose_encode(gt_cameras.R.float(), gt_cameras.T_uvz.float(), gt_cameras.focal_length.float(),
                                      _ratio(gt_cameras), B, S)
-        # ---- T_F ----
-        rgb_feat = F.add_rows(rgb_feat, self._table("1d", S, C, rgb_feat.device), S)
-        for blk in self.trunk:
-            rgb_feat = blk(rgb_feat)
         # ---- GAPR ----
         rot = self.pose_branch(rgb_feat)
         uv = F.linear(rgb_feat, self.fc_translation2d.weight, self.fc_translation2d.bias, out_dtype=torch.float32)
@@ -244,6 +256,28 @@ class CameraPredictor(nn.Module):
             pred_cameras = PredCameras(R=R, T=T, focal_length=torch.zeros(B * S, 0, device=R.device))
         out = {"pred_pose_enc": enc, "gt_pose_enc": gt_enc, "pred_cameras": pred_cameras}
         if gt_enc is not None:
+            out.update(loss=losses[0], loss_trans=losses[1], loss_rot=losses[2])
+        else:
+            out.update(loss=0, loss_trans=0, loss_rot=0)
+        return out
+
+    def _single_head(self, rgb_feat, gt_cameras, B, S):
+        """camera_predictor_abl_uvz.py:379-436 / _abl_all.py: one Mlp predicts (dxyz, q); q is
+        F.normalize'd, loss vs camera_to_pose_encoding3 (same weights / x100 MSE form as GAPR), frame 0
+        reset, pose_encoding_to_camera3 (focal 2.0). The fused GAPR kernels run on strided views
+        of the 7-wide output."""
+        pred = self.pose_branch(rgb_feat)  # [B, S, 7] f32
+        gt8 = None
+        if gt_cameras is not None:
+            gt8 = ops.pose_encode3(gt_cameras.R.float(), gt_cameras.T.float(), B, S)
+        enc, losses = F.gapr(pred[..., 3:7], pred[..., 0:2], pred[..., 2:3], gt8, B, S,
+                             self._cfg_get("weight_trans", 1.0), self._cfg_get("weight_rot", 2.0))
+        pred_cameras = None
+        if gt_cameras is not None:
+            R, T = ops.pose_decode3(enc, gt_cameras.R.float(), gt_cameras.T.float(), B, S)
+            pred_cameras = PredCameras(R=R, T=T, focal_length=torch.full((B * S, 1), 2.0, device=R.device))
+        out = {"pred_pose_enc": enc, "gt_pose_enc": None if gt8 is None else gt8[:, :7], "pred_cameras": pred_cameras}
+        if gt8 is not None:
             out.update(loss=losses[0], loss_trans=losses[1], loss_rot=losses[2])
         else:
             out.update(loss=0, loss_trans=0, loss_rot=0)

@@ -634,6 +634,22 @@ def pose_decode(enc, R_gt, T_gt, ratio, intr, B, S):
     return Rout, Tout
 
 
+def pose_encode3(R, T, B, S):
+    """camera_to_pose_encoding3 per sequence -> [B*S, 8] (column 7 zero padding)."""
+    enc = torch.empty(B * S, 8, device=R.device, dtype=torch.float32)
+    _chk(L.load().comet_pose_encode3(_p(R.contiguous()), _p(T.contiguous()), _p(enc), B, S, stream()), "pose_encode3")
+    return enc
+
+
+def pose_decode3(enc, R_gt, T_gt, B, S):
+    """pose_encoding_to_camera3 per sequence -> (R [B*S, 4], T [B*S, 3]) f32."""
+    Rout = torch.empty(B * S, 4, device=enc.device, dtype=torch.float32)
+    Tout = torch.empty(B * S, 3, device=enc.device, dtype=torch.float32)
+    _chk(L.load().comet_pose_decode3(_p(enc.contiguous()), _p(R_gt.contiguous()), _p(T_gt.contiguous()), _p(Rout),
+                                     _p(Tout), B, S, stream()), "pose_decode3")
+    return Rout, Tout
+
+
 # ------------------------------------------------------------------------------------------
 # tracker
 # ------------------------------------------------------------------------------------------

@@ -204,6 +204,47 @@ __global__ void pose_decode_kernel(const float* __restrict__ enc, const float* _
   }
 }
 
+// camera_to_pose_encoding3 per frame (utils.py:591-627, the single-head ablations abl_uvz /
+// abl_all): enc [rows, 8] = (T_i - T_0 (xyz), quaternion_multiply(q_i, q_0^-1), 0); frame 0 =
+// (0, 0, 0, 1, 0, 0, 0, 0). Column 7 is padding so the GAPR kernels read it like encoding 2.
+__global__ void pose_encode3_kernel(const float* __restrict__ R, const float* __restrict__ T,
+                                    float* __restrict__ enc, int64_t B, int S) {
+  GRID_STRIDE(t, B * S) {
+    const int64_t b = t / S;
+    const int s = (int)(t % S);
+    const float* r0 = R + b * S * 4;
+    const float* t0 = T + b * S * 3;
+    float* e = enc + t * 8;
+    e[7] = 0.f;
+    if (s == 0) {
+      e[0] = e[1] = e[2] = 0.f; e[3] = 1.f; e[4] = e[5] = e[6] = 0.f;
+      continue;
+    }
+    const float inv[4] = {r0[0], -r0[1], -r0[2], -r0[3]};
+    float q[4];
+    qmul_std(R + t * 4, inv, q);
+    const float* ti = T + t * 3;
+    e[0] = ti[0] - t0[0]; e[1] = ti[1] - t0[1]; e[2] = ti[2] - t0[2];
+    e[3] = q[0]; e[4] = q[1]; e[5] = q[2]; e[6] = q[3];
+  }
+}
+
+// pose_encoding_to_camera3 per frame (utils.py:270-310): R = quaternion_multiply(dq, q_0),
+// T = T_0 + dxyz (f32, the xyz translation of the sequence's frame 0).
+__global__ void pose_decode3_kernel(const float* __restrict__ enc, const float* __restrict__ Rgt,
+                                    const float* __restrict__ Tgt, float* __restrict__ Rout,
+                                    float* __restrict__ Tout, int64_t B, int S) {
+  GRID_STRIDE(t, B * S) {
+    const int64_t b = t / S;
+    const float* e = enc + t * 7;
+    const float* t0 = Tgt + b * S * 3;
+    Tout[t * 3 + 0] = t0[0] + e[0];
+    Tout[t * 3 + 1] = t0[1] + e[1];
+    Tout[t * 3 + 2] = t0[2] + e[2];
+    qmul_std(e + 3, Rgt + b * S * 4, Rout + t * 4);
+  }
+}
+
 // GAPR head (camera_predictor10.py:385-460). One block; rows t = b*S + s.
 // rot raw [rows,4] (ld_rot), uv [rows,2] (ld_uv), dd [rows,1] (ld_d), gt [rows,8] or NULL.
 // Outputs: qn [rows,4] normalized quats (pre-reset, kept for backward), enc [rows,7] with frame 0
@@ -411,6 +452,24 @@ extern "C" int comet_pose_decode(const float* enc, const float* R_gt, const floa
   hipLaunchKernelGGL(pose_decode_kernel, dim3(g1d(B * S)), dim3(256), 0, as_stream(stream), enc, R_gt, T_uvz_gt,
                      ratio, ratio_dev, fx, fy, cx, cy, R_out, T_out, B, S);
   COMET_CHECK_LAUNCH("comet_pose_decode");
+  return COMET_OK;
+}
+
+extern "C" int comet_pose_encode3(const float* R, const float* T, float* enc, int64_t B, int S, void* stream) {
+  COMET_CHECK_ARG(R && T && enc && S >= 1, "comet_pose_encode3: bad args");
+  if (B == 0) return COMET_OK;
+  hipLaunchKernelGGL(pose_encode3_kernel, dim3(g1d(B * S)), dim3(256), 0, as_stream(stream), R, T, enc, B, S);
+  COMET_CHECK_LAUNCH("comet_pose_encode3");
+  return COMET_OK;
+}
+
+extern "C" int comet_pose_decode3(const float* enc, const float* R_gt, const float* T_gt, float* R_out, float* T_out,
+                                  int64_t B, int S, void* stream) {
+  COMET_CHECK_ARG(enc && R_gt && T_gt && R_out && T_out && S >= 1, "comet_pose_decode3: bad args");
+  if (B == 0) return COMET_OK;
+  hipLaunchKernelGGL(pose_decode3_kernel, dim3(g1d(B * S)), dim3(256), 0, as_stream(stream), enc, R_gt, T_gt, R_out,
+                     T_out, B, S);
+  COMET_CHECK_LAUNCH("comet_pose_decode3");
   return COMET_OK;
 }
 

@@ -311,6 +311,13 @@ int comet_pose_decode(const float* enc, const float* R_gt, const float* T_uvz_gt
                       const double* ratio_dev, double fx,
                       double fy, double cx, double cy, float* R_out, double* T_out, int64_t B, int S,
                       void* stream);
+/* Single-head ablations (camera_predictor_abl_uvz.py / _abl_all.py): camera_to_pose_encoding3
+ * (utils.py:591-627) per sequence: enc [B*S,8] = (T_i - T_0 in xyz, q_i * q_0^-1 standardised,
+ * 0 padding; frame 0 = (0,0,0,1,0,0,0,0)) -- the GAPR kernels take it like encoding 2; and
+ * pose_encoding_to_camera3 (utils.py:270-310): enc [B*S,7] -> R = dq * q_0, T = T_0 + dxyz (f32). */
+int comet_pose_encode3(const float* R, const float* T, float* enc, int64_t B, int S, void* stream);
+int comet_pose_decode3(const float* enc, const float* R_gt, const float* T_gt, float* R_out, float* T_out,
+                       int64_t B, int S, void* stream);
 /* GAPR head + pose loss (camera_predictor10.py:385-460): F.normalize(rot, eps 1e-8), loss =
  * w_trans*100*MSE(uvd[1:]) + w_rot*100*MSE(q[1:]) (mean over sequences), frame-0 reset.
  * gt_enc may be NULL (no loss). qn [B*S,4] is kept for the backward. */

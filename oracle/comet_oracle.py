@@ -382,6 +382,95 @@ def camera_predictor(images_flat, B, P, gt=None, pred_trajectories=None, track_c
 
 
 # ----------------------------------------------------------------------------------------
+# ablation heads — camera_predictor_abl_{time,track,uvz,all}.py (abl_*.yaml), from rgb_feat
+# ----------------------------------------------------------------------------------------
+ABLATIONS = {
+    # (use T_P, add its result, time embedding + trunk, single 7-output head with encoding 3)
+    "ours": (True, True, True, False),     # camera_predictor10.py
+    "time": (True, True, False, False),    # camera_predictor_abl_time.py:364-381 (T_F commented out)
+    "track": (True, False, True, False),   # camera_predictor_abl_track.py:348 (residual commented out)
+    "uvz": (True, True, True, True),       # camera_predictor_abl_uvz.py:153, 379-436
+    "all": (False, False, False, True),    # camera_predictor_abl_all.py
+}
+
+
+def camera_to_pose_encoding3(R, T):
+    """utils.py:591-627 for one sequence: R [S,4], T (xyz) [S,3] -> [S,7]."""
+    S = R.shape[0]
+    enc = torch.zeros(S, 7)
+    enc[0, 3:7] = torch.tensor([1.0, 0.0, 0.0, 0.0])
+    for i in range(1, S):
+        enc[i, :3] = T[i] - T[0]
+        enc[i, 3:7] = quat_mul(R[i], quat_inv(R[0]))
+    return enc
+
+
+def pose_encoding_to_camera3(enc, R_ref, T_ref):
+    """utils.py:270-310 for one sequence: enc [S,7] -> (R = dq * q0, T = T0 + dxyz, focal 2.0)."""
+    n = enc.shape[0]
+    T = T_ref.unsqueeze(0).expand(n, 3) + enc[:, :3]
+    q = quat_mul(enc[:, 3:7], R_ref.unsqueeze(0).expand(n, 4))
+    return q, T, torch.full((n, 1), 2.0)
+
+
+def ablation_head(rgb_feat, P, variant, gt=None, pred_trajectories=None, track_confidence=None,
+                  intri_type="AMD_eval", pre="camera_predictor", heads=8):
+    """CameraPredictor.forward from rgb_feat_init for one of ABLATIONS (camera_predictor10.py:288-484
+    and the abl_* files): dict(pred_pose_enc [B*S,7], gt_pose_enc, loss, loss_trans, loss_rot,
+    pred_R, pred_T)."""
+    use_tp, tp_res, use_time, single = ABLATIONS[variant]
+    B, S, C = rgb_feat.shape
+    if use_tp and tp_res and pred_trajectories is not None:
+        t = linear(pred_trajectories, P, pre + ".traj_encoder.mlp.0")
+        t = F.layer_norm(t, (t.shape[-1],), P[pre + ".traj_encoder.mlp.1.weight"], P[pre + ".traj_encoder.mlp.1.bias"], 1e-5)
+        t = linear(F.relu(t), P, pre + ".traj_encoder.mlp.3")
+        t = F.layer_norm(t, (C,), P[pre + ".traj_encoder.mlp.4.weight"], P[pre + ".traj_encoder.mlp.4.bias"], 1e-5)
+        N = t.shape[2]
+        w = linear(track_confidence.unsqueeze(-1), P, pre + ".confidence_attention.0", "relu")
+        w = torch.sigmoid(linear(w, P, pre + ".confidence_attention.2"))
+        ctx = (t * w).reshape(B * S, N, C)
+        r = rgb_feat.reshape(B * S, 1, C)
+        for i in range(4):
+            r = cross_attn_block(r, ctx, P, f"{pre}.cross_attn_block.{i}", heads)
+        rgb_feat = rgb_feat + r.reshape(B, S, C)
+    if use_time:
+        rgb_feat = rgb_feat + sincos_1d(C, S).expand(B, -1, -1)
+        for i in range(4):
+            rgb_feat = attn_block(rgb_feat, P, f"{pre}.trunk.{i}", heads)
+    out = {}
+    if single:
+        pred = mlp(rgb_feat, P, pre + ".pose_branch")
+        uvd, rot = pred[..., :3], F.normalize(pred[..., 3:7], p=2, dim=-1, eps=1e-8)
+    else:
+        rot = F.normalize(mlp(rgb_feat, P, pre + ".pose_branch"), p=2, dim=-1, eps=1e-8)
+        uvd = torch.cat([linear(rgb_feat, P, pre + ".fc_translation2d"), linear(rgb_feat, P, pre + ".fc_depth")], -1)
+    if gt is not None:
+        if single:
+            encs = [camera_to_pose_encoding3(gt["R"][b * S:(b + 1) * S], gt["T"][b * S:(b + 1) * S]) for b in range(B)]
+        else:
+            encs = [camera_to_pose_encoding2(gt["R"][b * S:(b + 1) * S], gt["T_uvz"][b * S:(b + 1) * S],
+                                             gt["focal_length"][b * S:(b + 1) * S], gt["ratio"]) for b in range(B)]
+        loss, lt, lr = pose_loss(uvd, rot, encs)
+        out.update(loss=loss, loss_trans=lt, loss_rot=lr, gt_pose_enc=torch.cat(encs, 0))
+    uvd, rot = uvd.clone(), rot.clone()
+    uvd[:, 0, :] = 0
+    rot[:, 0, :] = torch.tensor([1.0, 0.0, 0.0, 0.0])
+    enc = torch.cat([uvd, rot], dim=-1)
+    out["pred_pose_enc"] = enc.reshape(-1, 7)
+    if gt is not None:
+        Rs, Ts = [], []
+        for b in range(B):
+            if single:
+                q, T, _ = pose_encoding_to_camera3(enc[b], gt["R"][b * S], gt["T"][b * S])
+            else:
+                q, T, _ = pose_encoding_to_camera2(enc[b], gt["R"][b * S], gt["T_uvz"][b * S], gt["ratio"], intri_type)
+            Rs.append(q)
+            Ts.append(T)
+        out["pred_R"], out["pred_T"] = torch.cat(Rs, 0), torch.cat(Ts, 0)
+    return out
+
+
+# ----------------------------------------------------------------------------------------
 # tracker CNNs — modules.py:39-116, blocks.py:27-202 (NCHW, InstanceNorm2d affine=False)
 # ----------------------------------------------------------------------------------------
 

@@ -504,6 +504,76 @@ def main_metrics():
     print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
 
 
+ABL_CFG = dict(B=1, S=4, N=16, seed_rgb=21, seed_x=1)
+
+
+def gen_ablations(out):
+    """SURVEY §8(f4) fixtures (tests/golden/comet_golden_abl.npz): the reference's ablation heads
+    (camera_predictor_abl_{time,track,uvz,all}.py, selected by abl_*.yaml) and camera_predictor10
+    itself, from a PRNG rgb_feat_init (the forward's own entry for precomputed image features,
+    camera_predictor_abl_*.py forward), PRNG tracks / confidences / GT cameras: outputs, losses,
+    decoded cameras and every parameter gradient's norm. Weights: oracle.prng per key name (same
+    values as the COMET goldens for shared keys)."""
+    H.install_stubs()
+    q = ABL_CFG
+    B, S, N = q["B"], q["S"], q["N"]
+    rgb = torch.from_numpy(prng.normal_like(q["seed_rgb"], "rgb_feat", (B, S, 768)))
+    _, tracks, gt = prng.synthetic_batch(q["seed_x"], B, S, 128, 128, N)
+    conf = torch.from_numpy((prng.uniform(q["seed_rgb"], "conf", (B, S, N)) + 1.0) * 0.5)
+    QC = H.reference_module("train_eval_func_new_cp5").QuaternionCameras
+    out["abl_cfg"] = np.array([B, S, N, q["seed_rgb"], q["seed_x"]])
+    out["abl_rgb"], out["abl_tracks"], out["abl_conf"] = np32(rgb), np32(tracks), np32(conf)
+    for v, (mod, yml) in {"ours": ("models.camera_predictor10", "abl_ours.yaml"),
+                          "time": ("models.camera_predictor_abl_time", "abl_time.yaml"),
+                          "track": ("models.camera_predictor_abl_track", "abl_track.yaml"),
+                          "uvz": ("models.camera_predictor_abl_uvz", "abl_uvz.yaml"),
+                          "all": ("models.camera_predictor_abl_all", "abl_all.yaml")}.items():
+        cfg = H.load_cfg(yml)
+        M = H.reference_module(mod)
+        M.CameraPredictor.get_backbone = lambda self, b: H.make_standin()
+        kw = {k: val for k, val in cfg.MODEL.CAMERA.items() if k != "_target_"}
+        torch.manual_seed(0)
+        cp = M.CameraPredictor(cfg=cfg, **kw)
+        shapes = {"camera_predictor." + k: tuple(t.shape) for k, t in cp.state_dict().items()
+                  if not k.startswith("backbone.")}
+        P = prng.make_state_dict(SEED_W, shapes)
+        cp.load_state_dict({k[len("camera_predictor."):]: t for k, t in P.items()}, strict=False)
+        cams = QC(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+                  principal_point=gt["principal_point"], ratio=gt["ratio"])
+        pred = cp(None, batch_size=B, rgb_feat_init=rgb, gt_cameras=cams, pred_trajectories=tracks,
+                  track_confidence=conf)
+        cp.zero_grad()
+        pred["loss"].backward()
+        grads = {k: p.grad for k, p in cp.named_parameters() if p.grad is not None}
+        pre = f"abl_{v}_"
+        out[pre + "pred_pose_enc"] = np32(pred["pred_pose_enc"])
+        out[pre + "gt_pose_enc"] = np32(pred["gt_pose_enc"])
+        for k in ("loss", "loss_trans", "loss_rot"):
+            out[pre + k] = np32(pred[k].reshape(1))
+        out[pre + "pred_R"] = np32(pred["pred_cameras"].R)
+        out[pre + "pred_T"] = np32(pred["pred_cameras"].T)
+        names = sorted(grads)
+        out[pre + "grad_names"] = np.array(names)
+        out[pre + "grad_norms"] = np.array([grads[k].double().norm().item() for k in names])
+        o = O.ablation_head(rgb, P, v, gt=gt, pred_trajectories=tracks, track_confidence=conf)
+        diffs = {"pred_pose_enc": (o["pred_pose_enc"] - pred["pred_pose_enc"]).abs().max().item(),
+                 "loss": abs(o["loss"].item() - pred["loss"].item()),
+                 "pred_R": (o["pred_R"] - pred["pred_cameras"].R).abs().max().item(),
+                 "pred_T": (o["pred_T"].double() - pred["pred_cameras"].T.double()).abs().max().item()}
+        print(v, "grads", len(names), "loss", float(pred["loss"]), "oracle vs reference:",
+              {k: f"{x:.2e}" for k, x in diffs.items()})
+
+
+def main_ablations():
+    H.require_reference()
+    torch.set_num_threads(8)
+    out = {}
+    gen_ablations(out)
+    path = os.path.join(OUT, "comet_golden_abl.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
 def main():
     H.require_reference()
     os.makedirs(OUT, exist_ok=True)
@@ -525,6 +595,8 @@ def main():
 if __name__ == "__main__":
     if "--v2" in sys.argv:
         main_v2()
+    elif "--ablations" in sys.argv:
+        main_ablations()
     elif "--metrics" in sys.argv:
         main_metrics()
     elif "--headline" in sys.argv:
