@@ -133,6 +133,9 @@ SIGNATURES = {
                                  ctypes.c_double, ctypes.c_double, c_vp, c_vp, c_i64, _INT, c_vp]),
     "comet_pose_encode3": (_INT, [c_vp, c_vp, c_vp, c_i64, _INT, c_vp]),
     "comet_pose_decode3": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_vp]),
+    "comet_resample_coeffs": (_INT, [_INT, _F, _F, _INT, c_vp, c_vp, _INT, ctypes.POINTER(_INT)]),
+    "comet_lanczos_crop_resize": (_INT, [c_vp, c_i64, _INT, _INT, c_i64, _INT, _INT, _INT, _INT, _INT, _INT, c_vp, c_vp,
+                                         _INT, c_vp, c_vp, _INT, _INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "comet_gapr_fwd": (_INT, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, _INT, _INT, _F, _F, c_vp]),
     "comet_gapr_bwd": (_INT, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, _INT, _INT,
                               _F, _F, c_vp]),

@@ -395,6 +395,26 @@ int comet_pose_pair_errors(const float* pred_w2v, const float* gt_w2v, int64_t b
 int comet_pose_frame_errors(const float* pred_enc, int64_t ld_pred, const float* gt_enc, int64_t ld_gt,
                             int64_t n, float* trans_deg, float* geo_rad, float* euler, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Data path (YTDataset.load_images_from_folder, kubric_movif_SFM_dataset_YT.py:236-266):
+ * PIL Image.crop (black outside the frame) + Image.resize(crop_size, LANCZOS) + ImageNet
+ * normalisation, byte-exact with Pillow's Resample.c.
+ * comet_resample_coeffs (host): Pillow's precompute_coeffs + normalize_coeffs_8bpc for LANCZOS
+ *   over the source span [in0, in1) of in_size pixels -> bounds [out_size*2] (first source pixel,
+ *   tap count), coeffs [out_size*max_ksize] int32 (22 fraction bits); coeffs == NULL: only the
+ *   table width *ksize.
+ * comet_lanczos_crop_resize (device): frames [n][h][w][3] uint8 (frame_stride bytes apart), crop
+ *   box origin (x0, y0) size (cw, ch), output (ow, oh): horizontal pass over crop rows
+ *   ybase .. ybase + rows - 1 (bx / kx, width ksx; skipped when ow == cw) into tmp
+ *   [n][rows][ow][3] uint8, vertical pass (by rebased to ybase / ky, width ksy; skipped when
+ *   oh == ch) -> out [n][3][oh][ow] f32 = (u / 255 - mean[c]) / std[c]. */
+int comet_resample_coeffs(int in_size, float in0, float in1, int out_size, int32_t* bounds, int32_t* coeffs,
+                          int max_ksize, int* ksize);
+int comet_lanczos_crop_resize(const uint8_t* frames, int64_t n, int h, int w, int64_t frame_stride, int x0, int y0,
+                              int cw, int ch, int ow, int oh, const int32_t* bx, const int32_t* kx, int ksx,
+                              const int32_t* by, const int32_t* ky, int ksy, int ybase, int rows, uint8_t* tmp,
+                              const float* mean, const float* stdv, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -564,6 +564,45 @@ def gen_ablations(out):
               {k: f"{x:.2e}" for k, x in diffs.items()})
 
 
+DATA_CASES = {"a": (0, "model0/seq_0", (64, 64), 4), "b": (5, "model0/seq_1", (64, 64), 4),
+              "c": (7, "model0/seq_0", (48, 80), 6), "d": (3, "model0/seq_1", (32, 32), 12)}
+
+
+def gen_data(out):
+    """SURVEY §8(f2) fixtures (tests/golden/comet_golden_data.npz): the reference's
+    YTDataset.load_images_from_folder (kubric_movif_SFM_dataset_YT.py:160-266) on the synthetic
+    sequences of tests/yt_fixture.py (PNG frames / masks, GT text), np.random seeded per case."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import yt_fixture
+    H.install_stubs()
+    Y = H.reference_module("kubric_movif_SFM_dataset_YT")
+    with tempfile.TemporaryDirectory() as root:
+        yt_fixture.make_dataset(root)
+        for tag, (seed, seq, crop, T) in DATA_CASES.items():
+            ds = Y.YTDataset(root, crop_size=crop, seq_len=T)
+            np.random.seed(seed)
+            smp = ds.load_images_from_folder(seq)
+            pre = f"d{tag}_"
+            out[pre + "cfg"] = np.array([seed, crop[0], crop[1], T])
+            out[pre + "seq"] = np.array(seq)
+            for k in ("images", "T", "R", "T_uvz", "R_matrix"):
+                out[pre + k] = np32(smp[k])
+            out[pre + "first_mask"] = smp["first_mask"].numpy()
+            out[pre + "ratio"] = np.array([smp["ratio"]], dtype=np.float64)
+            out[pre + "image_names"] = np.array(smp["image_names"])
+            print(tag, seq, tuple(smp["images"].shape), "ratio", smp["ratio"], smp["image_names"])
+
+
+def main_data():
+    H.require_reference()
+    out = {}
+    gen_data(out)
+    path = os.path.join(OUT, "comet_golden_data.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
 def main_ablations():
     H.require_reference()
     torch.set_num_threads(8)
@@ -597,6 +636,8 @@ if __name__ == "__main__":
         main_v2()
     elif "--ablations" in sys.argv:
         main_ablations()
+    elif "--data" in sys.argv:
+        main_data()
     elif "--metrics" in sys.argv:
         main_metrics()
     elif "--headline" in sys.argv:

@@ -9,6 +9,8 @@ pytorch3d, kornia, lightglue, cv2, imageio, torchvision) and the torch.hub DINOv
 import importlib
 import math
 import os
+
+import numpy as np
 import sys
 import types
 
@@ -82,7 +84,16 @@ def install_stubs():
     _mod("lightglue", SuperPoint=None, SIFT=None, ALIKED=None)
     _mod("train_util", check_ni=None, record_and_print_cpu_memory_and_usage=None,
          process_spark_data=None, process_spark_data2=None, set_seed_and_print=None)
-    _mod("cv2")
+    def find_nonzero(m):  # OpenCV findNonZero: (x, y) of the nonzero pixels, [n, 1, 2]
+        ys, xs = np.nonzero(m)
+        return np.stack([xs, ys], -1).reshape(-1, 1, 2).astype(np.int32)
+
+    def bounding_rect(pts):  # OpenCV boundingRect of a point set: (x, y, w, h), w = xmax - xmin + 1
+        p = pts.reshape(-1, 2)
+        x0, y0 = p.min(0)
+        return int(x0), int(y0), int(p[:, 0].max() - x0 + 1), int(p[:, 1].max() - y0 + 1)
+
+    _mod("cv2", findNonZero=find_nonzero, boundingRect=bounding_rect)
     _mod("imageio")
     _mod("visualizer", Visualizer=None)
     _mod("torchvision")
