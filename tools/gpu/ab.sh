@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B of an env switch on the bench line: bash tools/gpu/ab.sh <tag> <ENV=VALUE>
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
+O=gpurun_out/$1
+mkdir -p $O
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/a.json 2> $O/a.err || exit 1
+env $2 timeout -k 10 300 python bench.py --no-cpu-baseline > $O/b.json 2> $O/b.err || exit 1
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/a2.json 2> $O/a2.err || exit 1
+for f in a b a2; do python -c "import json;d=json.loads(open('$O/$f.json').read().strip().splitlines()[-1]);print('$f',d['value'],d['ms_per_step'])"; done
