@@ -106,6 +106,22 @@ typedef struct comet_rowln_args {
 int comet_gemm_rowln_ok(const comet_gemm_args* args);
 int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_args* ln, void* stream);
 
+/* Fused update-former MLP (Mlp fc1 -> GELU -> fc2 + residual, modules.py:119-154, 285-294,
+ * 334-343) with the row-LN epilogue of comet_gemm_rowln: v = resid + fc2(GELU(fc1(x))) per row,
+ * the [m, hidden] activation kept in LDS per 128-row block. x [m, c_dim] bf16 (ldx), w1 [hidden,
+ * c_dim] bf16, w2 [c_dim, hidden] bf16 (dense), b1 / b2 / resid / c f32; outputs as
+ * comet_rowln_args. Eligible (comet_mlp_rowln_ok): c_dim 256 or 384, hidden % 128 == 0. */
+typedef struct comet_mlp_args {
+  const void* x; int64_t ldx;
+  const void* w1; const float* b1;
+  const void* w2; const float* b2;
+  const float* resid; int64_t ldr;
+  float* c; int64_t ldc;
+  int64_t m; int32_t c_dim; int32_t hidden;
+} comet_mlp_args;
+int comet_mlp_rowln_ok(int64_t m, int c_dim, int hidden);
+int comet_mlp_rowln(const comet_mlp_args* args, const comet_rowln_args* ln, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM convolution on channels-last activations (nn.Conv2d of BasicEncoder /
  * ShallowEncoder / ResidualBlock, blocks.py:27-202, modules.py:39-116): the im2col matrix is

@@ -851,3 +851,37 @@ def test_gemm_rowln_matches_separate_kernels():
     _close(c, y32r, 1e-5, 1e-5, "rowln dual f32 vs separate")
     d = (y16.float() - y16r.float()).abs() / y16r.float().abs().clamp_min(1e-3)
     assert d.max().item() <= 2 ** -7, d.max().item()
+
+
+@pytest.mark.parametrize("mch", [(65536, 384, 1536), (16384 + 40, 384, 1536), (8192, 256, 1024), (300, 384, 1536)])
+@pytest.mark.parametrize("mode", ["raw_y16", "dual", "dual_ctx"])
+def test_mlp_rowln(mch, mode):
+    """comet_mlp_rowln (fused update-former Mlp: fc1 -> GELU -> fc2 + residual with the row-LN
+    epilogue; hidden tile in LDS) vs f64 with the hidden rounded to bf16 as the unfused path stores
+    it; M tails (rows beyond M are never written)."""
+    ops = _ops()
+    M, C, Hd = mch
+    x = _rand(M, C, seed=121).to(torch.bfloat16)
+    w1 = _rand(Hd, C, seed=122, scale=C ** -0.5).to(torch.bfloat16)
+    b1 = _rand(Hd, seed=123, scale=0.1)
+    w2 = _rand(C, Hd, seed=124, scale=Hd ** -0.5).to(torch.bfloat16)
+    b2 = _rand(C, seed=125, scale=0.1)
+    r = _rand(M, C, seed=126) + 0.25
+    zw, zb = _rand(C, seed=127), _rand(C, seed=128)
+    h = F.gelu(x.double() @ w1.double().t() + b1.double()).to(torch.bfloat16).double()
+    v = h @ w2.double().t() + b2.double() + r.double()
+    mu = v.mean(-1, keepdim=True)
+    var = v.var(-1, unbiased=False, keepdim=True)
+    ln6 = (v - mu) / torch.sqrt(var + 1e-6)
+    ln5 = (v - mu) / torch.sqrt(var + 1e-5) * zw.double() + zb.double()
+    d = lambda t: t.to(DEV)  # noqa: E731
+    raw = mode == "raw_y16"
+    c, y16, z16 = ops.mlp_rowln(d(x), d(w1), d(b1), d(w2), d(b2), d(r), raw=raw, y16_eps=1e-6,
+                                z=(d(zw), d(zb), 1e-5) if mode == "dual_ctx" else None)
+    torch.cuda.synchronize()
+    # the kernel's hidden is bf16-rounded GELU of an f32 accumulation: a few hidden values round the
+    # other way than the f64 reference's, each moving v by <= 2^-8 |h w2|
+    _close(c, v if raw else ln6, 1e-3, 2e-3, f"mlp c {mch} {mode}")
+    _close(y16, ln6, 1e-2, 1e-2, f"mlp y16 {mch} {mode}")
+    if mode == "dual_ctx":
+        _close(z16, ln5, 1e-2, 4e-2, f"mlp z16 {mch} {mode}")
