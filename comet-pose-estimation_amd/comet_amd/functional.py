@@ -278,6 +278,111 @@ class _LayerNormDual(torch.autograd.Function):
         return dx, None
 
 
+class _ResLayerNorm(torch.autograd.Function):
+    """(x, LN(x) non-affine in the compute dtype) for `x + Mlp(LN(x))` (modules.py:293-294,
+    342-343): the backward folds the residual branch's gradient into the LN backward kernel
+    (comet_layernorm_bwd_res) instead of autograd adding the two gradients of x in a separate pass."""
+
+    @staticmethod
+    def forward(ctx, x, eps):
+        y, mean, rstd = ops.layernorm(x, eps=eps, out_dtype=compute_dtype(), stats=True)
+        ctx.save_for_backward(x, mean, rstd)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, dres, dy):
+        x, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            return dres, None
+        if dres is None:
+            return ops.layernorm_bwd(x, dy, mean, rstd, dx_dtype=x.dtype), None
+        if x.dtype == torch.float32 and x.shape[-1] % 8 == 0:
+            return ops.layernorm_bwd_res(x, dy, dres, mean, rstd), None
+        return ops.layernorm_bwd(x, dy, mean, rstd, dx_dtype=x.dtype) + dres, None
+
+
+def res_layer_norm(x, eps=1e-6):
+    """(x, LN(x) in the compute dtype): the residual and the normed Mlp input of x + Mlp(LN(x))."""
+    if _needs_grad(x):
+        return _ResLayerNorm.apply(x, eps)
+    return x, ops.layernorm(x, eps=eps, out_dtype=compute_dtype())
+
+
+class _LinearPair(torch.autograd.Function):
+    """q = xq W[:C]^T + b[:C], kv = xkv W[C:]^T + b[C:] (the cross-attention in_proj of
+    nn.MultiheadAttention, modules.py:339): the backward writes both weight / bias gradient halves
+    straight into one [3C, C] / [3C] tensor -- autograd's slice backward would zero-fill a full
+    gradient per slice and add them."""
+
+    @staticmethod
+    def forward(ctx, xq, xkv, w, b, C):
+        ctx.cdt = compute_dtype()
+        wc = wcast(w, ctx.cdt)
+        xq2 = xq.reshape(-1, xq.shape[-1])
+        xkv2 = xkv.reshape(-1, xkv.shape[-1])
+        xq2 = xq2 if xq2.dtype == wc.dtype else ops.cast(xq2, wc.dtype)
+        xkv2 = xkv2 if xkv2.dtype == wc.dtype else ops.cast(xkv2, wc.dtype)
+        q = ops.linear(xq2, wc[:C], bias=b[:C], out_dtype=ctx.cdt)
+        kv = ops.linear(xkv2, wc[C:], bias=b[C:], out_dtype=ctx.cdt)
+        ctx.save_for_backward(xq2, xkv2, w)
+        ctx.C, ctx.shapes, ctx.dtypes = C, (xq.shape, xkv.shape), (xq.dtype, xkv.dtype)
+        return q.reshape(*xq.shape[:-1], C), kv.reshape(*xkv.shape[:-1], 2 * C)
+
+    @staticmethod
+    def backward(ctx, dq, dkv):
+        xq2, xkv2, w = ctx.saved_tensors
+        C = ctx.C
+        wc = wcast(w, ctx.cdt)
+        dw = torch.zeros(w.shape, device=w.device, dtype=torch.float32) if (dq is None or dkv is None) \
+            else torch.empty(w.shape, device=w.device, dtype=torch.float32)
+        db = torch.zeros(w.shape[0], device=w.device, dtype=torch.float32) if (dq is None or dkv is None) \
+            else torch.empty(w.shape[0], device=w.device, dtype=torch.float32)
+        grads = []
+        for d, x2, sl, shp, xdt in ((dq, xq2, slice(0, C), ctx.shapes[0], ctx.dtypes[0]),
+                                    (dkv, xkv2, slice(C, 3 * C), ctx.shapes[1], ctx.dtypes[1])):
+            if d is None:
+                grads.append(None)
+                continue
+            d2 = d.reshape(-1, d.shape[-1])
+            if not d2.is_contiguous():
+                d2 = d2.contiguous()
+            dx_dtype = xdt if ctx.cdt == torch.bfloat16 else torch.float32
+            dx = _linear_bwd_into(x2, wc[sl], d2, dw[sl], db[sl], dx_dtype, ctx.cdt)
+            dx = dx.reshape(shp)
+            grads.append(dx if dx.dtype == xdt else ops.cast(dx, xdt))
+        return grads[0], grads[1], dw, db, None
+
+
+def _linear_bwd_into(x2, wc, dy2, dw, db, dx_dtype, cdt):
+    """dx of y = x W^T + b, with dW / db written into the given (row-contiguous) views."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    if cdt == torch.bfloat16 and _vec8(dy2):
+        dpre = dy2 if dy2.dtype == torch.bfloat16 else ops.act_bwd_colsum(L.ACT_NONE, None, dy2,
+                                                                          out_dtype=torch.bfloat16, dbias=db)
+        if dy2.dtype == torch.bfloat16:
+            ops.act_bwd_colsum(L.ACT_NONE, None, dy2, dbias=db, want_out=False)
+    else:
+        dpre = dy2
+        db.copy_(ops.colsum(dpre))
+        if dpre.dtype != cdt:
+            dpre = ops.cast(dpre, cdt)
+    dx = torch.empty(M, K, device=dy2.device, dtype=dx_dtype)
+    ops.gemm_raw(dpre, wc, dx, m=M, n=K, k=N, layout_a=0, lda=dpre.stride(0), layout_b=1,
+                 ldb=wc.stride(0), ldc=K, compute=cdt)
+    xc = x2 if (x2.dtype == cdt or cdt == torch.bfloat16) else ops.cast(x2, cdt)
+    ops.gemm_raw(dpre, xc, dw, m=N, n=K, k=M, layout_a=1, lda=dpre.stride(0), layout_b=1,
+                 ldb=xc.stride(0), ldc=dw.stride(0), compute=cdt)
+    return dx
+
+
+def linear_pair(xq, xkv, w, b, C):
+    """(xq W[:C]^T + b[:C], xkv W[C:]^T + b[C:]) in the compute dtype (see _LinearPair)."""
+    if _needs_grad(xq, xkv, w, b):
+        return _LinearPair.apply(xq, xkv, w, b, C)
+    return linear(xq, w[:C], b[:C]), linear(xkv, w[C:], b[C:])
+
+
 def layer_norm(x, w=None, b=None, eps=1e-5, out_dtype=torch.float32):
     """nn.LayerNorm; out_dtype = compute dtype when the output only feeds a GEMM (the reference's
     autocast rounds it to bf16 at the Linear anyway)."""

@@ -195,18 +195,17 @@ class CameraPredictor(nn.Module):
         a = blk.attn
         x = tok.reshape(B * S, P, C)
         xn, xc = F.layer_norm_dual(x, eps=1e-6)  # every row: K / V need all of them
-        W, b = a.in_proj_weight, a.in_proj_bias
-        kv = F.linear(xc, W[C:], b[C:])  # [B*S, P, 2C]
         xc4, xn4 = xc.reshape(B, S, P, C), xn.reshape(B, S, P, C)
         # query rows: frame 0 (all P) then token 0 of every frame (frame 0's again: 1 row / sequence)
         qin = torch.cat([xc4[:, 0].reshape(B * P, C), xc4[:, :, 0].reshape(B * S, C)])
         rin = torch.cat([xn4[:, 0].reshape(B * P, C), xn4[:, :, 0].reshape(B * S, C)])
-        q = F.linear(qin, W[:C], b[:C])
+        q, kv = F.linear_pair(qin, xc, a.in_proj_weight, a.in_proj_bias, C)  # kv [B*S, P, 2C]
         o0 = F.attention(q[:B * P].reshape(B, P, C), kv.reshape(B, S, P, 2 * C)[:, 0], blk.heads, C)
         o1 = F.attention(q[B * P:].reshape(B * S, 1, C), kv, blk.heads, C)
         o = torch.cat([o0.reshape(B * P, C), o1.reshape(B * S, C)])
         y = F.linear(o, a.out_proj.weight, a.out_proj.bias, resid=rin, out_dtype=torch.float32)
-        y = blk.mlp(F.layer_norm(y, eps=1e-6, out_dtype=F.compute_dtype()), resid=y)
+        yr, yn = F.res_layer_norm(y, eps=1e-6)
+        y = blk.mlp(yn, resid=yr)
         f0 = y[:B * P].reshape(B, P, C)
         rows = y[B * P:].reshape(B, S, C)[:, 1:].contiguous()
         r = cblk(rows, f0)  # [B, S-1, C]

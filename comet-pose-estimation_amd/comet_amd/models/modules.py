@@ -57,7 +57,8 @@ class AttnBlock(nn.Module):
         qkv = F.linear(xc, a.in_proj_weight, a.in_proj_bias)
         o = F.attention(qkv, None, self.heads, C)
         x = F.linear(o, a.out_proj.weight, a.out_proj.bias, resid=x, out_dtype=torch.float32)
-        return self.mlp(F.layer_norm(x, eps=1e-6, out_dtype=F.compute_dtype()), resid=x)
+        xr, xn = F.res_layer_norm(x, eps=1e-6)
+        return self.mlp(xn, resid=xr)
 
 
 def _res_ln(x, w, b, resid, raw=True, y16_eps=None, z=None):
@@ -157,12 +158,11 @@ class CrossAttnBlock(nn.Module):
         x, xc = F.layer_norm_dual(x, eps=1e-6)
         ctx = F.layer_norm(context, self.norm_context.weight, self.norm_context.bias, eps=1e-5,
                            out_dtype=F.compute_dtype())
-        W, b = a.in_proj_weight, a.in_proj_bias
-        q = F.linear(xc, W[:C], b[:C])
-        kv = F.linear(ctx, W[C:], b[C:])
+        q, kv = F.linear_pair(xc, ctx, a.in_proj_weight, a.in_proj_bias, C)
         o = F.attention(q, kv, self.heads, C)
         x = F.linear(o, a.out_proj.weight, a.out_proj.bias, resid=x, out_dtype=torch.float32)
-        return self.mlp(F.layer_norm(x, eps=1e-6, out_dtype=F.compute_dtype()), resid=x)
+        xr, xn = F.res_layer_norm(x, eps=1e-6)
+        return self.mlp(xn, resid=xr)
 
 
 # ------------------------------------------------------------------------------------------

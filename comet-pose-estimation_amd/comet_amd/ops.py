@@ -361,6 +361,18 @@ def layernorm_bwd(x, dy, mean, rstd, weight=None, dweight=None, dbias=None, dx=N
     return dx
 
 
+def layernorm_bwd_res(x, dy, dres, mean, rstd, weight=None, dweight=None, dbias=None):
+    """dx (f32) = dres + LN backward of dy (x + f(LN(x)) without a separate gradient add)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    xc, dyc, drc = x.contiguous(), dy.contiguous(), dres.contiguous().float()
+    dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+    L.check(L.load().comet_layernorm_bwd_res(dt(xc), dt(dyc), _p(xc), _p(dyc), _p(drc), _p(mean), _p(rstd),
+                                             _p(weight), _p(dx), _p(dweight), _p(dbias), rows, C, stream()),
+            "layernorm_bwd_res")
+    return dx
+
+
 # ------------------------------------------------------------------------------------------
 # Attention
 # ------------------------------------------------------------------------------------------

@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(256)
 ln_bwd_vec_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const __bf16* __restrict__ dy2,
                   const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w,
                   TO* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db, int64_t rows, int cols,
-                  int accum) {
+                  int accum, const float* __restrict__ dres = nullptr) {
   __shared__ float red[2][4][1024];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float gw[NK][CH], gb[NK][CH], wv[NK][CH];
@@ -337,6 +337,12 @@ ln_bwd_vec_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const __b
         loadn<CH>(p, prev);
 #pragma unroll
         for (int e = 0; e < CH; ++e) o[e] += prev[e];
+      }
+      if (dres) {  // gradient of the residual branch that also reads x (x + f(LN(x)))
+        float r[CH];
+        loadn<CH>(dres + row * cols + c0, r);
+#pragma unroll
+        for (int e = 0; e < CH; ++e) o[e] += r[e];
       }
       storen<CH>(p, o);
     }
@@ -708,5 +714,35 @@ extern "C" int comet_instnorm_nhwc(int dtype, const void* x, const void* res, vo
                        (const __bf16*)res, (__bf16*)y, hw, (int)c, eps, relu, res_norm_relu);
   else { set_error("comet_instnorm_nhwc: bad dtype"); return COMET_EINVAL; }
   COMET_CHECK_LAUNCH("comet_instnorm_nhwc");
+  return COMET_OK;
+}
+
+// LayerNorm backward whose input also feeds a residual (x + Mlp(LN(x)), modules.py:293-294 /
+// 342-343): dx = dres + LN backward of dy in one pass (no separate gradient add).
+extern "C" int comet_layernorm_bwd_res(int dtype_x, int dtype_dy, const void* x, const void* dy, const float* dres,
+                                       const float* mean, const float* rstd, const float* weight, float* dx,
+                                       float* dweight, float* dbias, int64_t rows, int64_t cols, void* stream) {
+  COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_bwd_res: cols must be in [1,1024]");
+  COMET_CHECK_ARG(x && dy && dres && mean && rstd && dx, "comet_layernorm_bwd_res: null pointer");
+  COMET_CHECK_ARG(cols % 8 == 0 && a32(x) && a32(dy) && a32(dres) && a32(dx),
+                  "comet_layernorm_bwd_res: needs cols % 8 == 0 and 32-B aligned rows");
+  if (rows == 0) return COMET_OK;
+  dim3 grid((unsigned)cdiv(rows, 4 * LN_RPW));
+  hipStream_t s = as_stream(stream);
+#define LBR(TX, TD, NK)                                                                                          \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TX, TD, float, 4, NK>), grid, dim3(256), 0, s, (const TX*)x, (const TD*)dy, \
+                     (const __bf16*)nullptr, mean, rstd, weight, dx, dweight, dbias, rows, (int)cols, 0, dres)
+#define LBR_NK(TX, TD)                                                            \
+  do {                                                                            \
+    const int nk = (int)cdiv(cols, 64 * 4);                                       \
+    if (nk == 1) LBR(TX, TD, 1); else if (nk == 2) LBR(TX, TD, 2);               \
+    else if (nk == 3) LBR(TX, TD, 3); else LBR(TX, TD, 4);                        \
+  } while (0)
+  if (dtype_x == COMET_F32 && dtype_dy == COMET_F32) LBR_NK(float, float);
+  else if (dtype_x == COMET_F32 && dtype_dy == COMET_BF16) LBR_NK(float, __bf16);
+  else { set_error("comet_layernorm_bwd_res: x must be f32"); return COMET_EINVAL; }
+#undef LBR_NK
+#undef LBR
+  COMET_CHECK_LAUNCH("comet_layernorm_bwd_res");
   return COMET_OK;
 }

@@ -165,6 +165,11 @@ int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy
                         const float* mean, const float* rstd, const float* weight,
                         int dtype_dx, void* dx, float* dweight, float* dbias, int64_t rows, int64_t cols,
                         int dx_accumulate, void* stream);
+/* x + f(LN(x)) (modules.py:293-294, 342-343): dx (f32) = dres + LN backward of dy, one pass
+ * (x f32, dy f32 / bf16, cols % 8 == 0, 32-B aligned rows). */
+int comet_layernorm_bwd_res(int dtype_x, int dtype_dy, const void* x, const void* dy, const float* dres,
+                            const float* mean, const float* rstd, const float* weight, float* dx,
+                            float* dweight, float* dbias, int64_t rows, int64_t cols, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused multi-head attention forward (flash style: LDS-staged K/V, online softmax, MFMA for
