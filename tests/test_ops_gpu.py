@@ -885,3 +885,19 @@ def test_mlp_rowln(mch, mode):
     _close(y16, ln6, 1e-2, 1e-2, f"mlp y16 {mch} {mode}")
     if mode == "dual_ctx":
         _close(z16, ln5, 1e-2, 4e-2, f"mlp z16 {mch} {mode}")
+
+
+@pytest.mark.parametrize("mnk", [(8192, 1536, 384), (4096 + 72, 3072, 768), (65536, 1024, 256)])
+@pytest.mark.parametrize("act", [1, 2])
+def test_gemm_persistent_preact_bf16(mnk, act):
+    """Persistent kernel, bf16 output with an activation and no aux: bias + activation applied to
+    the accumulators before the parked whole-line stores (PREACT), M tails; vs f64."""
+    ops = _ops()
+    M, N, K = mnk
+    x = _rand(M, K, seed=131).to(torch.bfloat16)
+    w = _rand(N, K, seed=132, scale=K ** -0.5).to(torch.bfloat16)
+    b = _rand(N, seed=133)
+    pre = x.double() @ w.double().t() + b.double()
+    ref = F.gelu(pre) if act == 1 else torch.relu(pre)
+    out = ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=act, out_dtype=torch.bfloat16)
+    _close(out, ref, 1e-2, 1e-2, f"pp preact {mnk} act{act}")
