@@ -148,6 +148,10 @@ SIGNATURES = {
     "comet_resample_coeffs": (_INT, [_INT, _F, _F, _INT, c_vp, c_vp, _INT, ctypes.POINTER(_INT)]),
     "comet_lanczos_crop_resize": (_INT, [c_vp, c_i64, _INT, _INT, c_i64, _INT, _INT, _INT, _INT, _INT, _INT, c_vp, c_vp,
                                          _INT, c_vp, c_vp, _INT, _INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "comet_sp_preprocess": (_INT, [_INT, c_vp, c_vp, _INT, _INT, _INT, _INT, _INT, _INT, c_vp]),
+    "comet_maxpool2_nhwc": (_INT, [_INT, c_vp, c_vp, c_i64, _INT, _INT, _INT, c_vp]),
+    "comet_sp_scores": (_INT, [c_vp, c_vp, _INT, _INT, _INT, c_vp]),
+    "comet_maxfilt2d": (_INT, [c_vp, c_vp, c_vp, _INT, _INT, _INT, _INT, c_vp]),
     "comet_gapr_fwd": (_INT, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, _INT, _INT, _F, _F, c_vp]),
     "comet_gapr_bwd": (_INT, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, _INT, _INT,
                               _F, _F, c_vp]),

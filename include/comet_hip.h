@@ -436,6 +436,23 @@ int comet_lanczos_crop_resize(const uint8_t* frames, int64_t n, int h, int w, in
                               const int32_t* by, const int32_t* ky, int ksy, int ybase, int rows, uint8_t* tmp,
                               const float* mean, const float* stdv, float* out, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Keypoint initialisation (train_eval_func_new_cp5.py:527-595: lightglue SuperPoint.extract on
+ * frame 0, then filter_and_pad): the SuperPoint encoder / detector convolutions run on
+ * comet_conv2d_nhwc; these are its other dense stages.
+ * comet_sp_preprocess: x [B,3,H,W] f32 -> bilinear (align_corners=False) resize to OH x OW
+ *   (up-sampling only) + grayscale (0.299, 0.587, 0.114) -> y [B,OH,OW,cpad] (channel 0; rest 0).
+ * comet_maxpool2_nhwc: nn.MaxPool2d(2, 2) on NHWC.
+ * comet_sp_scores: detector logits [B,h,w,65] f32 -> softmax, dustbin dropped, depth-to-space
+ *   -> scores [B, 8h, 8w].
+ * comet_maxfilt2d: (2r+1)^2 stride-1 max filter of [B,H,W] f32 (max_pool2d with padding r),
+ *   tmp = B*H*W floats of workspace (simple_nms; filter_and_pad's 3x3 mask dilation). */
+int comet_sp_preprocess(int dtype_y, const float* x, void* y, int B, int H, int W, int OH, int OW, int cpad,
+                        void* stream);
+int comet_maxpool2_nhwc(int dtype, const void* x, void* y, int64_t n, int H, int W, int C, void* stream);
+int comet_sp_scores(const float* logits, float* scores, int B, int h, int w, void* stream);
+int comet_maxfilt2d(const float* x, float* y, float* tmp, int B, int H, int W, int r, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -471,6 +471,30 @@ def ablation_head(rgb_feat, P, variant, gt=None, pred_trajectories=None, track_c
 
 
 # ----------------------------------------------------------------------------------------
+# keypoint initialisation helpers
+# ----------------------------------------------------------------------------------------
+def simple_nms(scores, r):
+    """LightGlue simple_nms / glue-factory batched_nms (superpoint_open.py:34-48) on [B, H, W]."""
+    mp = lambda t: F.max_pool2d(t, kernel_size=2 * r + 1, stride=1, padding=r)  # noqa: E731
+    zeros = torch.zeros_like(scores)
+    max_mask = scores == mp(scores)
+    for _ in range(2):
+        supp = mp(max_mask.float()) > 0
+        supp_scores = torch.where(supp, zeros, scores)
+        max_mask = max_mask | ((supp_scores == mp(supp_scores)) & ~supp)
+    return torch.where(max_mask, scores, zeros)
+
+
+def filter_keypoints(pts, mask):
+    """RNG-free part of filter_and_pad (train_eval_func_new_cp5.py:272-282): keypoints whose rounded,
+    clamped pixel lies in the mask, in input order."""
+    H, W = mask.shape
+    xs = pts[:, 0].round().clamp(0, W - 1).long()
+    ys = pts[:, 1].round().clamp(0, H - 1).long()
+    return pts[mask.bool()[ys, xs]]
+
+
+# ----------------------------------------------------------------------------------------
 # tracker CNNs — modules.py:39-116, blocks.py:27-202 (NCHW, InstanceNorm2d affine=False)
 # ----------------------------------------------------------------------------------------
 

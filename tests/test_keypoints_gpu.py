@@ -1,0 +1,119 @@
+"""SURVEY §8(f1) keypoint initialisation on the GPU: the SuperPoint NMS (comet_maxfilt2d) and
+filter_and_pad vs fixtures from the reference tree (tests/golden/comet_golden_kp.npz), the
+detector-head decode / max pooling / preprocessing kernels vs torch fp32 references, and an
+extract() + keypoint_tracks run (random weights: LightGlue's superpoint_v1.pth is not available
+offline, so detections are unpinned -- checked for shape, range and count)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as TF
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(ROOT, "tests", "golden", "comet_golden_kp.npz")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return dict(np.load(GOLD, allow_pickle=False))
+
+
+def test_nms_matches_reference(gold):
+    from comet_amd.keypoints import simple_nms
+    for t in "abc":
+        got = simple_nms(torch.from_numpy(gold[f"nms{t}_in"]).cuda(), int(gold[f"nms{t}_r"][0]))
+        np.testing.assert_array_equal(got.cpu().numpy(), gold[f"nms{t}_out"])
+
+
+def test_filter_and_pad_matches_reference(gold):
+    from comet_amd.keypoints import filter_and_pad
+    for t in "ab":
+        lo, hi = (int(v) for v in gold[f"fp{t}_cfg"])
+        got = filter_and_pad(torch.from_numpy(gold[f"fp{t}_pts"]).cuda(), torch.from_numpy(gold[f"fp{t}_mask"]).cuda(),
+                             lo, hi)
+        np.testing.assert_array_equal(got.cpu().numpy(), gold[f"fp{t}_out"])
+
+
+def test_filter_and_pad_random_branches():
+    """Padding from the mask, then its 1-px ring, then anywhere; random subset above max_pts."""
+    from comet_amd.keypoints import filter_and_pad
+    torch.manual_seed(0)
+    H, W = 40, 50
+    m = torch.zeros(H, W, dtype=torch.bool, device="cuda")
+    m[10:20, 15:30] = True
+    pts = torch.tensor([[20.0, 12.0], [1.0, 1.0]], device="cuda")
+    out = filter_and_pad(pts, m, 64, 100)
+    assert out.shape == (64, 2) and torch.equal(out[0], pts[0])
+    xs, ys = out[:, 0].long(), out[:, 1].long()
+    assert bool(m[ys, xs].all())
+    tiny = torch.zeros(H, W, dtype=torch.bool, device="cuda")
+    tiny[5, 5] = True  # one pixel: padding draws from it with replacement, then nothing else needed
+    out2 = filter_and_pad(pts, tiny, 10, 20)
+    assert out2.shape == (10, 2)
+    empty = torch.zeros(H, W, dtype=torch.bool, device="cuda")
+    out3 = filter_and_pad(pts, empty, 10, 20)  # no mask: random pixels of the frame
+    assert out3.shape == (10, 2) and bool((out3[:, 0] < W).all()) and bool((out3[:, 1] < H).all())
+    many = torch.rand(500, 2, device="cuda") * torch.tensor([W - 1.0, H - 1.0], device="cuda")
+    full = torch.ones(H, W, dtype=torch.bool, device="cuda")
+    out4 = filter_and_pad(many, full, 10, 128)
+    assert out4.shape == (128, 2)
+
+
+def test_sp_scores_and_pool_match_torch():
+    from comet_amd import _lib as L
+    from comet_amd import ops
+    from comet_amd.keypoints import sp_scores
+    g = torch.Generator().manual_seed(5)
+    lg = torch.randn(2, 6, 7, 65, generator=g) * 3
+    got = sp_scores(lg.cuda()).cpu()
+    p = torch.softmax(lg.permute(0, 3, 1, 2), 1)[:, :-1]
+    ref = p.permute(0, 2, 3, 1).reshape(2, 6, 7, 8, 8).permute(0, 1, 3, 2, 4).reshape(2, 48, 56)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-7)
+    x = torch.randn(3, 10, 12, 64, generator=g).cuda()
+    y = torch.empty(3, 5, 6, 64, device="cuda")
+    L.check(L.load().comet_maxpool2_nhwc(L.F32, x.data_ptr(), y.data_ptr(), 3, 10, 12, 64, ops.stream()), "pool")
+    ref = TF.max_pool2d(x.permute(0, 3, 1, 2), 2, 2).permute(0, 2, 3, 1)
+    assert torch.equal(y, ref)
+
+
+def test_sp_preprocess_matches_torch():
+    from comet_amd.keypoints import SuperPoint
+    g = torch.Generator().manual_seed(6)
+    img = torch.randn(1, 3, 40, 56, generator=g).cuda()
+    sp = SuperPoint().cuda()
+    from comet_amd import functional as F
+    with F.precision(torch.float32):
+        y = sp._preprocess(img, 80, 112)
+    up = TF.interpolate(img, size=(80, 112), mode="bilinear", align_corners=False)
+    gray = (up * torch.tensor([0.299, 0.587, 0.114], device="cuda").view(1, 3, 1, 1)).sum(1)
+    torch.testing.assert_close(y[..., 0], gray, rtol=1e-5, atol=1e-5)
+    assert bool((y[..., 1:] == 0).all())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_superpoint_extract_and_tracks(dtype):
+    from comet_amd import functional as F
+    from comet_amd.keypoints import SuperPoint, keypoint_tracks
+    torch.manual_seed(0)
+    sp = SuperPoint(max_num_keypoints=512, detection_threshold=0.005).cuda()
+    with torch.no_grad():
+        for m in sp.modules():  # random weights with a usable score range (no checkpoint offline)
+            if isinstance(m, torch.nn.Conv2d):
+                torch.nn.init.kaiming_normal_(m.weight)
+                torch.nn.init.zeros_(m.bias)
+    g = torch.Generator().manual_seed(7)
+    imgs = torch.randn(2, 4, 3, 128, 160, generator=g).cuda()
+    with F.precision(dtype):
+        out = sp.extract(imgs[0, 0])
+        kp = out["keypoints"]
+        assert kp.shape[0] == 1 and kp.shape[-1] == 2 and 0 < kp.shape[1] <= 512
+        assert bool((kp[..., 0] >= -0.5).all()) and bool((kp[..., 0] <= 159.5).all())
+        assert bool((kp[..., 1] >= -0.5).all()) and bool((kp[..., 1] <= 127.5).all())
+        sc = out["keypoint_scores"][0]
+        assert bool((sc[:-1] >= sc[1:]).all()) and bool((sc > 0.005).all())
+        mask = torch.ones(2, 128, 160, dtype=torch.bool, device="cuda")
+        tracks, vis = keypoint_tracks(sp, imgs, mask, track_num=64, min_required=64)
+        assert tracks.shape == (2, 4, 64, 2) and vis.shape == (2, 4, 64) and bool(vis.all())

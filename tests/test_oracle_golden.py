@@ -264,3 +264,15 @@ def test_ablation_targets_resolve(variant):
     C = resolve_target(f"models.camera_predictor_abl_{variant}.CameraPredictor")
     assert C.__module__ == f"comet_amd.models.camera_predictor_abl_{variant}"
     assert C.SINGLE_HEAD == (variant in ("uvz", "all"))
+
+
+def test_oracle_keypoint_helpers_match_reference():
+    """oracle.simple_nms vs glue-factory's batched_nms and oracle.filter_keypoints vs
+    the reference's filter_and_pad (RNG-free cases), tests/golden/comet_golden_kp.npz."""
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "comet_golden_kp.npz"), allow_pickle=False))
+    for t in "abc":
+        got = O.simple_nms(torch.from_numpy(g[f"nms{t}_in"])[:, None], int(g[f"nms{t}_r"][0]))[:, 0]
+        np.testing.assert_array_equal(got.numpy(), g[f"nms{t}_out"])
+    for t in "ab":
+        got = O.filter_keypoints(torch.from_numpy(g[f"fp{t}_pts"]), torch.from_numpy(g[f"fp{t}_mask"]))
+        np.testing.assert_array_equal(got.numpy(), g[f"fp{t}_out"])

@@ -603,6 +603,55 @@ def main_data():
     print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
 
 
+def gen_keypoints(out):
+    """SURVEY §8(f1) fixtures (tests/golden/comet_golden_kp.npz): glue-factory's batched_nms (the
+    reference tree's copy of LightGlue's simple_nms, gluefactory/models/extractors/superpoint_open.py)
+    on score maps with plateaus, and the reference's filter_and_pad
+    (train_eval_func_new_cp5.py:261-314) on keypoint sets whose kept count needs no random padding
+    or subsetting (the RNG-free branch; the random branches are checked by property)."""
+    import importlib.util
+    import types
+    H.install_stubs()
+    # load superpoint_open.py alone: its package imports (base_model -> OmegaConf) are stubbed
+    for name in ("gluefactory", "gluefactory.models", "gluefactory.models.extractors", "gluefactory.models.utils"):
+        mod = types.ModuleType(name)
+        mod.__path__ = []
+        sys.modules.setdefault(name, mod)
+    sys.modules["gluefactory.models.base_model"] = types.SimpleNamespace(BaseModel=torch.nn.Module)
+    sys.modules["gluefactory.models.utils.misc"] = types.SimpleNamespace(pad_and_stack=None)
+    path = os.path.join(H.REF, "gluefactory", "models", "extractors", "superpoint_open.py")
+    spec = importlib.util.spec_from_file_location("gluefactory.models.extractors.superpoint_open", path)
+    sp_mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sp_mod)
+    batched_nms = sp_mod.batched_nms
+    g = torch.Generator().manual_seed(31)
+    for tag, (B, Hh, Ww, r) in {"a": (2, 48, 64, 4), "b": (1, 40, 40, 1), "c": (1, 33, 70, 2)}.items():
+        sc = torch.rand(B, Hh, Ww, generator=g)
+        sc = torch.where(sc < 0.3, torch.zeros_like(sc), (sc * 8).floor() / 8)  # plateaus and ties
+        out[f"nms{tag}_in"] = sc.numpy()
+        out[f"nms{tag}_r"] = np.array([r])
+        out[f"nms{tag}_out"] = batched_nms(sc, r).numpy()
+    T = H.reference_module("train_eval_func_new_cp5")
+    for tag, (Hh, Ww, n, lo, hi) in {"a": (64, 80, 300, 10, 400), "b": (50, 50, 120, 5, 200)}.items():
+        pts = torch.rand(n, 2, generator=g) * torch.tensor([Ww + 6.0, Hh + 6.0]) - 3.0
+        m = torch.zeros(Hh, Ww, dtype=torch.bool)
+        m[Hh // 5:Hh * 3 // 4, Ww // 4:Ww * 4 // 5] = True
+        kept = T.filter_and_pad(pts, m, lo, hi, "fixture")
+        out[f"fp{tag}_pts"], out[f"fp{tag}_mask"] = pts.numpy(), m.numpy()
+        out[f"fp{tag}_cfg"] = np.array([lo, hi])
+        out[f"fp{tag}_out"] = kept.numpy()
+        print("filter_and_pad", tag, tuple(kept.shape))
+
+
+def main_keypoints():
+    H.require_reference()
+    out = {}
+    gen_keypoints(out)
+    path = os.path.join(OUT, "comet_golden_kp.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
 def main_ablations():
     H.require_reference()
     torch.set_num_threads(8)
@@ -638,6 +687,8 @@ if __name__ == "__main__":
         main_ablations()
     elif "--data" in sys.argv:
         main_data()
+    elif "--keypoints" in sys.argv:
+        main_keypoints()
     elif "--metrics" in sys.argv:
         main_metrics()
     elif "--headline" in sys.argv:
