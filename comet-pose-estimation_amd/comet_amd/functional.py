@@ -11,6 +11,8 @@ Precision policy (mirrors accelerate mixed_precision="bf16" autocast, abl_ours.y
 """
 import contextlib
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -381,6 +383,44 @@ def linear_pair(xq, xkv, w, b, C):
     if _needs_grad(xq, xkv, w, b):
         return _LinearPair.apply(xq, xkv, w, b, C)
     return linear(xq, w[:C], b[:C]), linear(xkv, w[C:], b[C:])
+
+
+class _FrameSplit(torch.autograd.Function):
+    """tok [B, S, P, C] -> (tok[:, 0:1], tok[:, 0], tok[:, 1:]) as views: the per-layer split of
+    get_2D_image_features (camera_predictor10.py:663-683: frame 0 is both kept and the cross-attention
+    context, frames 1.. are the queries). One backward node assembles d tok with a single copy of the
+    frames-1.. gradient -- autograd's select / slice backwards would zero-fill three full-size
+    gradients and add them."""
+
+    @staticmethod
+    def forward(ctx, tok):
+        ctx.shape, ctx.dtype = tok.shape, tok.dtype
+        return tok[:, 0:1], tok[:, 0], tok[:, 1:]
+
+    @staticmethod
+    def backward(ctx, d_t0, d_f0, d_fo):
+        dtok = torch.empty(ctx.shape, device=(d_fo if d_fo is not None else d_f0 if d_f0 is not None else d_t0).device,
+                           dtype=ctx.dtype)
+        if d_fo is not None:
+            dtok[:, 1:].copy_(d_fo)
+        else:
+            dtok[:, 1:].zero_()
+        if d_t0 is not None and d_f0 is not None:
+            torch.add(d_t0[:, 0], d_f0, out=dtok[:, 0])
+        elif d_t0 is not None:
+            dtok[:, 0].copy_(d_t0[:, 0])
+        elif d_f0 is not None:
+            dtok[:, 0].copy_(d_f0)
+        else:
+            dtok[:, 0].zero_()
+        return dtok
+
+
+def frame_split(tok):
+    """(tok[:, 0:1], tok[:, 0], tok[:, 1:]) with one backward node (see _FrameSplit)."""
+    if _needs_grad(tok) and not os.environ.get("COMET_NO_FRAME_SPLIT"):
+        return _FrameSplit.apply(tok)
+    return tok[:, 0:1], tok[:, 0], tok[:, 1:]
 
 
 def layer_norm(x, w=None, b=None, eps=1e-5, out_dtype=torch.float32):

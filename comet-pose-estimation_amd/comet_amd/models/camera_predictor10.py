@@ -175,10 +175,9 @@ class CameraPredictor(nn.Module):
             if idx == self.att_depth - 1 and S > 1 and self.prune_dead_rows:
                 return self._last_layer_token0(tok, B, S, P, C), B, S, C
             tok = self.self_att[idx](tok.reshape(B * S, P, C)).reshape(B, S, P, C)
-            f0 = tok[:, 0]
-            fo = tok[:, 1:].reshape(B, (S - 1) * P, C)
-            fo = self.cross_att[idx](fo, f0).reshape(B, S - 1, P, C)
-            tok = torch.cat([tok[:, 0:1], fo], dim=1)
+            t0, f0, fo = F.frame_split(tok)
+            fo = self.cross_att[idx](fo.reshape(B, (S - 1) * P, C), f0).reshape(B, S - 1, P, C)
+            tok = torch.cat([t0, fo], dim=1)
         return tok[:, :, 0].contiguous(), B, S, C
 
     def _last_layer_token0(self, tok, B, S, P, C):

@@ -23,10 +23,11 @@ def refine_track(images, fine_fnet, fine_tracker, coarse_pred, pradius=15, sradi
     cdt = F.compute_dtype()
     patches, topleft, query = ops.patch_gather(images, coarse_pred, pradius, cdt,
                                                cpad=8 if cdt == torch.bfloat16 else 3)
-    feat = fine_fnet(patches)  # [B*N*S, P, P, 32]
+    feat, feat1 = fine_fnet(patches, with_pool=True)  # [B*N*S, P, P, 32], its 2x2 average pool
     P, C = feat.shape[1], feat.shape[-1]
     feat = feat.reshape(B * N, S, P, P, C)
-    preds, _, _, qfeat, _ = fine_tracker(query.reshape(B * N, 1, 2), fmaps=feat, iters=fine_iters, return_feat=True)
+    preds, _, _, qfeat, _ = fine_tracker(query.reshape(B * N, 1, 2), fmaps=feat, iters=fine_iters, return_feat=True,
+                                         pyramid1=feat1)
     fine_last = preds[-1].reshape(B * N, S, 2)
     refined = ops.refine_combine(fine_last, topleft, coarse_pred, B, S, N)
     score = inv = None

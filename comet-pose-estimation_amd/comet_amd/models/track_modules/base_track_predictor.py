@@ -61,7 +61,7 @@ class BaseTrackerPredictor(nn.Module):
 
     @torch.no_grad()
     def forward(self, query_points, fmaps=None, iters=4, return_feat=False, down_ratio=1, is_train=False,
-                track_feats=None, TRACKorPOSE=False, ind=0):
+                track_feats=None, TRACKorPOSE=False, ind=0, pyramid1=None):
         """query_points [B, N, 2]; fmaps NHWC [B, S, HH, WW, C] (compute dtype).
         Returns (coord_preds list of [B, S, N, 2], vis [B, S, N] or None, track_feats [B, N, S, C],
         query_track_feat [B, N, C], conf None)."""
@@ -77,7 +77,9 @@ class BaseTrackerPredictor(nn.Module):
         query_feat = ops.sample_bilinear(fm0, q, border=True)  # [B, N, C]
         track_feats = query_feat.reshape(B, N, 1, C).repeat(1, 1, S, 1).contiguous()  # f32 [B, N, S, C]
         pyr = [fmaps.reshape(B * S, HH, WW, C)]
-        for _ in range(self.corr_levels - 1):
+        if pyramid1 is not None and self.corr_levels > 1:  # level 1 already pooled by the producer
+            pyr.append(pyramid1)
+        while len(pyr) < self.corr_levels:
             pyr.append(ops.avgpool2_nhwc(pyr[-1]))
         pos = ops.sample_bilinear(self._pos_table(HH, WW, dev).expand(B, -1, -1, -1), q, border=True)  # [B, N, tdim]
         td = self.transformer_dim

@@ -8,6 +8,8 @@ im2col + MFMA GEMM, InstanceNorm/ReLU/residual tails are fused kernels.
   ShallowEncoder blocks.py:114-196  fine patch feature net -> [n, 31, 31, 32]
   EfficientUpdateFormer blocks.py:205-348 (time / virtual-track space attention)
 """
+import os
+
 import torch
 import torch.nn as nn
 
@@ -86,8 +88,9 @@ class ShallowEncoder(nn.Module):
         return ResidualBlock(self.in_planes, dim, self.norm_fn, stride=stride)
 
     @torch.no_grad()
-    def forward(self, x):
-        """x NHWC [n, P, P, 3] -> NHWC [n, P/stride, P/stride, 32]."""
+    def forward(self, x, with_pool=False):
+        """x NHWC [n, P, P, 3] -> NHWC [n, P/stride, P/stride, 32] (with_pool: also its 2x2 average
+        pool, the fine correlation pyramid's level 1, written by the same up-sampling kernel)."""
         _, H, W, _ = x.shape
         x = ops.instnorm_nhwc(conv2d_nhwc(x, self.conv1, 2, 1), relu=True)
         h, w = x.shape[1], x.shape[2]
@@ -98,7 +101,16 @@ class ShallowEncoder(nn.Module):
         n, _, _, c = x.shape
         x = F.linear(x.reshape(-1, c), F.wcast(self.conv2.weight.reshape(c, c)), self.conv2.bias,
                      resid=x.reshape(-1, c), out_dtype=x.dtype).reshape(n, h, w, c)
-        return ops.resize_bilinear(x, H // self.stride, W // self.stride, nhwc=True)
+        oh, ow = H // self.stride, W // self.stride
+        if with_pool:
+            # opt-in (COMET_RESIZE_POOL=1): the fused up-sample + pool kernel measured 0.7 ms/step slower
+            # than the two passes it replaces (profiles/r02_glue/ab2.txt)
+            r = ops.resize_pool_nhwc(x, oh, ow) if os.environ.get("COMET_RESIZE_POOL") else None
+            if r is not None:
+                return r
+            y = ops.resize_bilinear(x, oh, ow, nhwc=True)
+            return y, ops.avgpool2_nhwc(y)
+        return ops.resize_bilinear(x, oh, ow, nhwc=True)
 
 
 class EfficientUpdateFormer(nn.Module):

@@ -562,6 +562,25 @@ def resize_bilinear(x, oh, ow, nhwc, out=None, add=False, out_dtype=None):
     return out
 
 
+def resize_pool_nhwc(x, oh, ow):
+    """(resize_bilinear(x, oh, ow) NHWC, its 2x2 average pool) in one pass (comet_resize_pool_nhwc);
+    None when the images do not fit the one-workgroup-per-image kernel."""
+    n, h, w, c = x.shape
+    es = x.element_size()
+    if c % 8 or h * w * c * es > 32768:
+        return None
+    xc = x.contiguous()
+    y = torch.empty(n, oh, ow, c, device=x.device, dtype=x.dtype)
+    p = torch.empty(n, oh // 2, ow // 2, c, device=x.device, dtype=x.dtype)
+    e0 = PROF.start()
+    L.check(L.load().comet_resize_pool_nhwc(dt(xc), dt(y), _p(xc), _p(y), _p(p), n, c, h, w, oh, ow, stream()),
+            "resize_pool_nhwc")
+    if e0 is not None:
+        PROF.stop(e0, f"resize_pool [{n}x{h}x{w}x{c}]" if PROF.detail else "comet_resize_pool_nhwc", 0.0,
+                  float(es * (n * h * w * c + y.numel() + p.numel())))
+    return y, p
+
+
 def cast_multi_f32_bf16(srcs, dsts):
     """dst[i].copy_(src[i]) f32 -> bf16 (contiguous, equal numel) in few launches."""
     n = len(srcs)

@@ -290,6 +290,11 @@ int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, const void* x, 
 /* NHWC resize into a channel slice of a wider NHWC tensor (output pixel pitch ldy elements):
  * BasicEncoder's four up-sampled maps land directly in their torch.cat(dim=1) positions
  * (blocks.py:97-107), so the 416-channel concat is never copied. c, ldy % 8 == 0. */
+/* NHWC align_corners resize (as comet_resize_bilinear) that also writes the 2x2 average pool of its
+ * output: ShallowEncoder's final up-sample + the fine pyramid's first level (blocks.py:199-202,
+ * CorrBlock pyramid), one workgroup per image (input image <= 32 KiB of LDS), c % 8 == 0. */
+int comet_resize_pool_nhwc(int dtype_in, int dtype_out, const void* x, void* y, void* p, int64_t n, int64_t c,
+                           int64_t h, int64_t w, int64_t oh, int64_t ow, void* stream);
 int comet_resize_bilinear_nhwc_into(int dtype_in, int dtype_out, const void* x, void* y, int64_t n,
                                     int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
                                     int64_t ldy, int add, void* stream);

@@ -234,6 +234,7 @@ def test_e2e_fp32_intermediates_match_reference(setup, gold):
 
     def hook(name):
         def f(m, i, o):
+            o = o[0] if isinstance(o, tuple) else o  # fine_fnet(with_pool=True) also returns its pooled level
             cap[name] = (o["x_norm_patchtokens"] if isinstance(o, dict) else o).detach().clone()
         return f
     cp, tp = model.camera_predictor, model.track_predictor

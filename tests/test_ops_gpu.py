@@ -901,3 +901,15 @@ def test_gemm_persistent_preact_bf16(mnk, act):
     ref = F.gelu(pre) if act == 1 else torch.relu(pre)
     out = ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=act, out_dtype=torch.bfloat16)
     _close(out, ref, 1e-2, 1e-2, f"pp preact {mnk} act{act}")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_resize_pool_equals_resize_then_avgpool(dtype):
+    """comet_resize_pool_nhwc (ShallowEncoder up-sample + the fine pyramid's first avg-pool in one
+    pass) is bit-identical to comet_resize_bilinear followed by comet_avgpool2_nhwc."""
+    ops = _ops()
+    x = _rand(300, 16, 16, 32, seed=141, dtype=dtype).to(DEV)
+    y, p = ops.resize_pool_nhwc(x, 31, 31)
+    y_ref = ops.resize_bilinear(x, 31, 31, nhwc=True)
+    p_ref = ops.avgpool2_nhwc(y_ref)
+    assert torch.equal(y, y_ref) and torch.equal(p, p_ref)
