@@ -21,6 +21,7 @@
 // GEMMs: K = all tokens of the batch), blockIdx.z splits K; every split writes an f32 partial tile
 // into the caller's workspace and a second kernel sums the splits in a fixed order (deterministic)
 // and applies the epilogue.
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -1520,12 +1521,35 @@ bool pp_ok(const comet_gemm_args& a) {
 // Tile of the persistent kernel: 128 x 384 for N = 384 (the tracker's hidden size: each A row
 // block read once), else 256 x 256; half-height (64 x 384, 128 x 256) when the full-height tiles
 // leave CUs idle (M = 8192: the tracker's virtual tracks x frames x batch).
-void pp_tile(const comet_gemm_args& a, int& tbm, int& tbn) {
+void pp_tile_base(const comet_gemm_args& a, int& tbm, int& tbn) {
   int cus = num_cus();
   cus -= cus % 8;
   tbn = a.n == 384 ? 384 : 256;
   tbm = a.n == 384 ? 128 : 256;
   if (cdiv(a.m, tbm) * cdiv(a.n, tbn) < cus) tbm /= 2;
+}
+
+// plain GEMMs: the base tile, or COMET_PP_TILE=256x256 | 128x256 | 128x384 | 64x384 (measurement
+// override, tools/tile_bench.py)
+void pp_tile(const comet_gemm_args& a, int& tbm, int& tbn) {
+  pp_tile_base(a, tbm, tbn);
+  // small M (the tracker's virtual tracks, M = 8192): when 128 x 384 tiles fill 75-100 % of the
+  // CUs in one round they beat the 1.5-round 128 x 256 grid (N = 1536: 23.7 vs 30.1 us; N = 1152:
+  // 19.6 vs 22.8 us; profiles/r02_tile)
+  int cus = num_cus();
+  cus -= cus % 8;
+  const int64_t t384 = cdiv(a.m, 128) * (a.n / 384);
+  if (a.n != 384 && a.n % 384 == 0 && 4 * t384 >= 3 * (int64_t)cus && t384 <= cus && getenv("COMET_PP_NO_384") == nullptr) {
+    tbm = 128;
+    tbn = 384;
+  }
+  if (const char* t = getenv("COMET_PP_TILE")) {
+    int m = 0, n = 0;
+    if (sscanf(t, "%dx%d", &m, &n) == 2 && ((n == 256 && (m == 256 || m == 128)) || (n == 384 && (m == 128 || m == 64)))) {
+      tbm = m;
+      tbn = n;
+    }
+  }
 }
 
 // Row-LN launch (comet_gemm_rowln): f32 output with a residual, no activation / aux, one tile
@@ -1535,7 +1559,7 @@ int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s
   int grid = num_cus();
   grid -= grid % 8;
   int tbm, tbn;
-  pp_tile(a, tbm, tbn);
+  pp_tile_base(a, tbm, tbn);
   // tile rows: full-height 128 x 384 only for long K (K >= 1024: fc2), else the half-height tiles
   // (the full-height LN instances run at 256 VGPRs with spills; tools/rowln_bench.py)
   const bool full = tbn == 384 && a.k >= 1024 && getenv("COMET_ROWLN_HALF") == nullptr;
@@ -2086,7 +2110,7 @@ static bool rowln_ok(const comet_gemm_args& a, const comet_rowln_args* ln) {
   if (!pp_ok(a) || a.dtype_c != COMET_F32 || a.resid == nullptr || a.aux != nullptr || a.act != COMET_ACT_NONE) return false;
   if (a.n != 384 && a.n != 256) return false;
   int tbm, tbn;
-  pp_tile(a, tbm, tbn);
+  pp_tile_base(a, tbm, tbn);
   if (tbn != a.n) return false;
   if (ln == nullptr) return true;
   auto b4 = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 8 == 0 && ld % 4 == 0); };

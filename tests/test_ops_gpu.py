@@ -521,7 +521,7 @@ def test_gemm_256_tile_path(mnk, epi):
 
 @pytest.mark.parametrize("mnk", [(20000, 3072, 192), (70001, 768, 64), (33000, 1152, 256), (4100, 1024, 1536),
                                  (20001, 384, 1536), (8200, 384, 384), (65536, 384, 64),
-                                 (8192, 1536, 384), (6000, 768, 192)])
+                                 (8192, 1536, 384), (6000, 768, 192), (8200, 1152, 320)])
 @pytest.mark.parametrize("epi", ["plain_f32", "gelu_aux_bf16", "bias_resid_f32", "inplace_resid_f32"])
 def test_gemm_persistent_path(mnk, epi):
     """Persistent kernel (256 x 256 tiles; 128 x 384 for N = 384): several tiles per workgroup
@@ -550,6 +550,26 @@ def test_gemm_persistent_path(mnk, epi):
         else:
             out = ops.linear(xd, wd, bias=bd, resid=rd, beta=0.5, out_dtype=torch.float32)
         _close(out, pre + b.double() + 0.5 * r.double(), 1e-4, 1e-4 * math.sqrt(K), f"pp resid {mnk}")
+
+
+@pytest.mark.parametrize("tile", ["256x256", "128x256", "128x384", "64x384"])
+@pytest.mark.parametrize("mnk", [(5000, 1000, 192), (9000, 1536, 384)])
+def test_gemm_persistent_tiles(tile, mnk, monkeypatch):
+    """Every tile instance of the persistent kernel (COMET_PP_TILE override) on M / N tails (N = 1000
+    leaves a partial 384- and 256-column tile), GELU bf16 and residual f32 epilogues, vs f64."""
+    ops = _ops()
+    monkeypatch.setenv("COMET_PP_TILE", tile)
+    M, N, K = mnk
+    x = _rand(M, K, seed=98).to(torch.bfloat16)
+    w = _rand(N, K, seed=99, scale=0.1).to(torch.bfloat16)
+    b = _rand(N, seed=100)
+    r = _rand(M, N, seed=101)
+    pre = x.double() @ w.double().t() + b.double()
+    xd, wd, bd = x.to(DEV), w.to(DEV), b.to(DEV)
+    out = ops.linear(xd, wd, bias=bd, act=1, out_dtype=torch.bfloat16)
+    _close(out, F.gelu(pre), 1e-2, 1e-2, f"pp {tile} gelu {mnk}")
+    out = ops.linear(xd, wd, bias=bd, resid=r.to(DEV), out_dtype=torch.float32)
+    _close(out, pre + r.double(), 1e-4, 1e-4 * math.sqrt(K), f"pp {tile} resid {mnk}")
 
 
 @pytest.mark.parametrize("la,lb", [(0, 1), (1, 0), (1, 1)])
