@@ -395,7 +395,10 @@ class _FrameSplit(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tok):
         ctx.shape, ctx.dtype = tok.shape, tok.dtype
-        return tok[:, 0:1], tok[:, 0], tok[:, 1:]
+        # frames 1.. as one contiguous copy: the consumers (LayerNorm forward and backward of the
+        # cross-attention block) would each make it contiguous otherwise
+        fo = tok[:, 1:]
+        return tok[:, 0:1], tok[:, 0], (fo if _FRAME_VIEWS else fo.contiguous())
 
     @staticmethod
     def backward(ctx, d_t0, d_f0, d_fo):
@@ -414,6 +417,30 @@ class _FrameSplit(torch.autograd.Function):
         else:
             dtok[:, 0].zero_()
         return dtok
+
+
+class _FrameJoin(torch.autograd.Function):
+    """cat([t0, fo], dim=1) whose backward hands out the frames-1.. gradient as one contiguous
+    copy (autograd's CatBackward gives a strided view, which the cross-attention block's Linear and
+    residual-LayerNorm backwards would each copy)."""
+
+    @staticmethod
+    def forward(ctx, t0, fo):
+        return torch.cat([t0, fo], dim=1)
+
+    @staticmethod
+    def backward(ctx, d):
+        return d[:, 0:1], d[:, 1:].contiguous()
+
+
+_FRAME_VIEWS = bool(os.environ.get("COMET_FRAME_VIEWS"))  # A/B switch: strided frames-1.. views, plain cat
+
+
+def frame_join(t0, fo):
+    """torch.cat([t0, fo], dim=1) (see _FrameJoin)."""
+    if _needs_grad(t0, fo) and not os.environ.get("COMET_NO_FRAME_SPLIT") and not _FRAME_VIEWS:
+        return _FrameJoin.apply(t0, fo)
+    return torch.cat([t0, fo], dim=1)
 
 
 def frame_split(tok):

@@ -177,7 +177,7 @@ class CameraPredictor(nn.Module):
             tok = self.self_att[idx](tok.reshape(B * S, P, C)).reshape(B, S, P, C)
             t0, f0, fo = F.frame_split(tok)
             fo = self.cross_att[idx](fo.reshape(B, (S - 1) * P, C), f0).reshape(B, S - 1, P, C)
-            tok = torch.cat([t0, fo], dim=1)
+            tok = F.frame_join(t0, fo)
         return tok[:, :, 0].contiguous(), B, S, C
 
     def _last_layer_token0(self, tok, B, S, P, C):

@@ -47,6 +47,28 @@ def main():
         key = (ev.name, site)
         agg[key][0] += 1
         agg[key][1] += ev.device_time_total / 1e3
+    # backward ops run on the autograd engine's thread (no Python stack): name the autograd node
+    # (parent "autograd::engine::evaluate_function: XBackward") and the op's input shapes instead
+    byshape = collections.defaultdict(lambda: [0, 0.0])
+    for ev in prof.events():
+        if not ev.name.startswith("aten::") or ev.device_time_total <= 0:
+            continue
+        node, p = "fwd", ev.cpu_parent
+        while p is not None:
+            if p.name.startswith("autograd::engine::evaluate_function"):
+                node = p.name.split(":")[-1].strip()
+                break
+            if p.cpu_parent is None:
+                node = "fwd:" + p.name
+            p = p.cpu_parent
+        if ev.cpu_parent is not None and ev.cpu_parent.name.startswith("aten::"):
+            continue  # count each kernel once, at its outermost aten op
+        key = (ev.name, node, str(ev.input_shapes)[:90])
+        byshape[key][0] += 1
+        byshape[key][1] += ev.device_time_total / 1e3
+    print("by autograd node / input shapes:")
+    for (name, node, shp), (n, ms) in sorted(byshape.items(), key=lambda kv: -kv[1][1])[:40]:
+        print(f"{ms:8.3f} ms {n:5d}x  {name:22s} {node:34s} {shp}")
     rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
     tot = sum(v[1] for _, v in rows)
     print(f"torch aten kernels: {tot:.2f} ms")
