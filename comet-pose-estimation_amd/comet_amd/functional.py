@@ -433,6 +433,32 @@ class _FrameJoin(torch.autograd.Function):
         return d[:, 0:1], d[:, 1:].contiguous()
 
 
+class _GatherRows(torch.autograd.Function):
+    """x2 [R, C] -> x2[idx] with one backward node: a zero gradient and one index_add_ of the
+    gathered rows' gradients (repeated rows accumulate), instead of per-view select / slice
+    backwards that each zero-fill a full-size gradient and are then added."""
+
+    @staticmethod
+    def forward(ctx, x2, idx):
+        ctx.save_for_backward(idx)
+        ctx.rows = x2.shape[0]
+        return x2.index_select(0, idx)
+
+    @staticmethod
+    def backward(ctx, d):
+        (idx,) = ctx.saved_tensors
+        dx = torch.zeros(ctx.rows, d.shape[1], device=d.device, dtype=d.dtype)
+        dx.index_add_(0, idx, d)
+        return dx, None
+
+
+def gather_rows(x2, idx):
+    """x2[idx] over the rows of a 2-D tensor (see _GatherRows)."""
+    if _needs_grad(x2):
+        return _GatherRows.apply(x2, idx)
+    return x2.index_select(0, idx)
+
+
 _FRAME_VIEWS = bool(os.environ.get("COMET_FRAME_VIEWS"))  # A/B switch: strided frames-1.. views, plain cat
 
 

@@ -180,6 +180,15 @@ class CameraPredictor(nn.Module):
             tok = F.frame_join(t0, fo)
         return tok[:, :, 0].contiguous(), B, S, C
 
+    @staticmethod
+    def _query_rows(B, S, P, dev):
+        """Row indices into [B*S*P] of frame 0's P rows of every sequence, then token 0 of every
+        frame (the surviving query rows of _last_layer_token0)."""
+        b = torch.arange(B, device=dev)
+        f0 = (b[:, None] * (S * P) + torch.arange(P, device=dev)[None]).reshape(-1)
+        t0 = (b[:, None] * (S * P) + torch.arange(S, device=dev)[None] * P).reshape(-1)
+        return torch.cat([f0, t0])
+
     def _last_layer_token0(self, tok, B, S, P, C):
         """The last (self_att, cross_att) pair computing only the rows that survive (SURVEY
         Appendix B-8, camera_predictor10.py:666-687): only token 0 of every frame is returned, so
@@ -194,10 +203,10 @@ class CameraPredictor(nn.Module):
         a = blk.attn
         x = tok.reshape(B * S, P, C)
         xn, xc = F.layer_norm_dual(x, eps=1e-6)  # every row: K / V need all of them
-        xc4, xn4 = xc.reshape(B, S, P, C), xn.reshape(B, S, P, C)
         # query rows: frame 0 (all P) then token 0 of every frame (frame 0's again: 1 row / sequence)
-        qin = torch.cat([xc4[:, 0].reshape(B * P, C), xc4[:, :, 0].reshape(B * S, C)])
-        rin = torch.cat([xn4[:, 0].reshape(B * P, C), xn4[:, :, 0].reshape(B * S, C)])
+        idx = self._query_rows(B, S, P, x.device)
+        qin = F.gather_rows(xc.reshape(B * S * P, C), idx)
+        rin = F.gather_rows(xn.reshape(B * S * P, C), idx)
         q, kv = F.linear_pair(qin, xc, a.in_proj_weight, a.in_proj_bias, C)  # kv [B*S, P, 2C]
         o0 = F.attention(q[:B * P].reshape(B, P, C), kv.reshape(B, S, P, 2 * C)[:, 0], blk.heads, C)
         o1 = F.attention(q[B * P:].reshape(B * S, 1, C), kv, blk.heads, C)
