@@ -1294,6 +1294,22 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 #pragma unroll
           for (int t = 0; t < NTC; ++t) load4(epi.bias + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(bcp + t * CPL));
         }
+        // residual rows are loaded one (i, h) step ahead, so each step's HBM latency overlaps the
+        // previous step's park / reduce / store work instead of being exposed MI x 2 times
+        auto rload = [&](int ih, float (&dst)[NTC][CPL]) {
+          const int64_t row = prow0 + (ih >> 1) * 16 + (ih & 1) * 8;
+#pragma unroll
+          for (int t = 0; t < NTC; ++t)
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) dst[t][e] = 0.f;
+          if constexpr (HASR) {
+#pragma unroll
+            for (int t = 0; t < NTC; ++t)
+              if (!EDGE || row < M) loadn<CPL>(R + row * epi.ldr + pc0 + t * 8 * CPL, dst[t]);
+          }
+        };
+        float rcur[NTC][CPL];
+        rload(0, rcur);
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           float vh[2][NV];
@@ -1301,16 +1317,12 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
           for (int h = 0; h < 2; ++h) {
             const int64_t row = prow0 + i * 16 + h * 8;
             const bool live = !EDGE || row < M;
-            float rc[NTC][CPL];
+            float rc[NTC][CPL], rnext[NTC][CPL];
 #pragma unroll
             for (int t = 0; t < NTC; ++t)
 #pragma unroll
-              for (int e = 0; e < CPL; ++e) rc[t][e] = 0.f;
-            if constexpr (HASR) {
-#pragma unroll
-              for (int t = 0; t < NTC; ++t)
-                if (live) loadn<CPL>(R + row * epi.ldr + pc0 + t * 8 * CPL, rc[t]);
-            }
+              for (int e = 0; e < CPL; ++e) rc[t][e] = rcur[t][e];
+            if (2 * i + h + 1 < 2 * MI) rload(2 * i + h + 1, rnext);
             if ((li >> 3) == h) {
 #pragma unroll
               for (int j = 0; j < NI; ++j)
@@ -1339,6 +1351,12 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
             sq = red8(sq);
             if (cc == 0) *reinterpret_cast<float2*>(st + 2 * (lrow(i, h) + wc)) = float2{s, sq};
             asm volatile("" ::: "memory");
+            if (2 * i + h + 1 < 2 * MI) {
+#pragma unroll
+              for (int t = 0; t < NTC; ++t)
+#pragma unroll
+                for (int e = 0; e < CPL; ++e) rcur[t][e] = rnext[t][e];
+            }
           }
 #pragma unroll
           for (int h = 0; h < 2; ++h)
