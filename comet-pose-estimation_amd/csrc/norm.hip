@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(256)
 ln_bwd_vec_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const __bf16* __restrict__ dy2,
                   const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w,
                   TO* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db, int64_t rows, int cols,
-                  int accum, const float* __restrict__ dres = nullptr) {
+                  int accum, const float* __restrict__ dres = nullptr, int rpw = LN_RPW) {
   __shared__ float red[2][4][1024];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float gw[NK][CH], gb[NK][CH], wv[NK][CH];
@@ -288,8 +288,8 @@ ln_bwd_vec_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const __b
       gw[k][e] = 0.f; gb[k][e] = 0.f;
       wv[k][e] = (w && c < cols) ? w[c] : 1.f;
     }
-  const int64_t rbase = ((int64_t)blockIdx.x * 4 + wid) * LN_RPW;
-  for (int rr = 0; rr < LN_RPW; ++rr) {
+  const int64_t rbase = ((int64_t)blockIdx.x * 4 + wid) * rpw;
+  for (int rr = 0; rr < rpw; ++rr) {
     const int64_t row = rbase + rr;
     if (row >= rows) break;
     const float mu = mean[row], rs = rstd[row];
@@ -616,6 +616,18 @@ extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, cons
   return COMET_OK;
 }
 
+// rows per wave of the LayerNorm backward: with affine gradients every workgroup ends in
+// 2 x cols atomics, so waves take 16 rows; without them 2 rows per wave put more waves (and so
+// more rows' loads) in flight: 184 -> 137 us (dual) and 219 -> 158 us (residual) at 69240 x 768,
+// 4.0 -> 5.4 TB/s (tools/lnbwd_bench.py, profiles/r02_lnbwd). COMET_LNB_RPW overrides.
+static int ln_bwd_rpw(const float* dweight, const float* dbias) {
+  if (const char* e = getenv("COMET_LNB_RPW")) {
+    const int v = atoi(e);
+    if (v >= 1 && v <= 64) return v;
+  }
+  return (dweight || dbias) ? LN_RPW : 2;
+}
+
 extern "C" int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy, const void* dy2,
                                    const float* mean, const float* rstd, const float* weight,
                                    int dtype_dx, void* dx, float* dweight, float* dbias, int64_t rows,
@@ -623,13 +635,15 @@ extern "C" int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, con
   COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_bwd: cols must be in [1,1024]");
   COMET_CHECK_ARG(x && dy && mean && rstd && dx, "comet_layernorm_bwd: null pointer");
   if (rows == 0) return COMET_OK;
-  dim3 grid((unsigned)cdiv(rows, 4 * LN_RPW));
+  const int rpw = ln_bwd_rpw(dweight, dbias);
+  dim3 grid((unsigned)cdiv(rows, 4 * rpw));
   hipStream_t s = as_stream(stream);
   const bool vec = cols % 8 == 0 && a32(x) && a32(dy) && a32(dy2) && a32(dx);
   if (vec) {
 #define LBV(TX, TD, TO, CH, NK)                                                                           \
   hipLaunchKernelGGL((ln_bwd_vec_kernel<TX, TD, TO, CH, NK>), grid, dim3(256), 0, s, (const TX*)x, (const TD*)dy, \
-                     (const __bf16*)dy2, mean, rstd, weight, (TO*)dx, dweight, dbias, rows, (int)cols, dx_accumulate)
+                     (const __bf16*)dy2, mean, rstd, weight, (TO*)dx, dweight, dbias, rows, (int)cols, dx_accumulate, \
+                     nullptr, rpw)
 #define LBV_CH(TX, TD, TO, CH)                                                                             \
   do {                                                                                                     \
     const int nk = (int)cdiv(cols, 64 * CH);                                                               \
@@ -727,11 +741,12 @@ extern "C" int comet_layernorm_bwd_res(int dtype_x, int dtype_dy, const void* x,
   COMET_CHECK_ARG(cols % 8 == 0 && a32(x) && a32(dy) && a32(dres) && a32(dx),
                   "comet_layernorm_bwd_res: needs cols % 8 == 0 and 32-B aligned rows");
   if (rows == 0) return COMET_OK;
-  dim3 grid((unsigned)cdiv(rows, 4 * LN_RPW));
+  const int rpw = ln_bwd_rpw(dweight, dbias);
+  dim3 grid((unsigned)cdiv(rows, 4 * rpw));
   hipStream_t s = as_stream(stream);
 #define LBR(TX, TD, NK)                                                                                          \
   hipLaunchKernelGGL((ln_bwd_vec_kernel<TX, TD, float, 4, NK>), grid, dim3(256), 0, s, (const TX*)x, (const TD*)dy, \
-                     (const __bf16*)nullptr, mean, rstd, weight, dx, dweight, dbias, rows, (int)cols, 0, dres)
+                     (const __bf16*)nullptr, mean, rstd, weight, dx, dweight, dbias, rows, (int)cols, 0, dres, rpw)
 #define LBR_NK(TX, TD)                                                            \
   do {                                                                            \
     const int nk = (int)cdiv(cols, 64 * 4);                                       \
