@@ -540,6 +540,84 @@ in_apply_kernel(const T* __restrict__ x, const T* __restrict__ res, T* __restric
   in_block_apply(xb, res ? res + n * g.hw * g.c : nullptr, y + n * g.hw * g.c, g, p0, p1, st[0], st[1]);
 }
 
+// Small bf16 images (the fine ShallowEncoder: 65536 images of 16x16 / 8x8 / 4x4 x 32): one wave
+// per image holds the whole image in registers (NP 16-B vectors per lane), so the statistics need
+// no LDS / barrier (xor shuffles over the lanes of one channel group) and the apply pass no second
+// read; 4 images per workgroup. Same shifted-moment statistics as in_block_stats.
+template <int NP>
+__global__ void __launch_bounds__(256)
+in_wave_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ res, __bf16* __restrict__ y, int64_t n,
+               INGeo g) {
+  const int lane = threadIdx.x & 63;
+  const int64_t img = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (img >= n) return;
+  const int tpp = g.c / 8, ppw = 64 / tpp;
+  const int cg = lane % tpp, slot = lane / tpp;
+  const int hw = (int)g.hw;
+  const __bf16* xb = x + img * g.hw * g.c;
+  uint4 raw[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int p = slot + k * ppw;
+    raw[k] = p < hw ? *reinterpret_cast<const uint4*>(xb + (int64_t)p * g.c + cg * 8) : uint4{0, 0, 0, 0};
+  }
+  float K[8];
+  load8(xb + cg * 8, K);
+  auto unpack = [](const uint4& u, float (&v)[8]) {
+    v[0] = bf16_lo(u.x); v[1] = bf16_hi(u.x); v[2] = bf16_lo(u.y); v[3] = bf16_hi(u.y);
+    v[4] = bf16_lo(u.z); v[5] = bf16_hi(u.z); v[6] = bf16_lo(u.w); v[7] = bf16_hi(u.w);
+  };
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    if (slot + k * ppw >= hw) break;
+    float v[8];
+    unpack(raw[k], v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = v[e] - K[e];
+      s1[e] += d;
+      s2[e] += d * d;
+    }
+  }
+  const float inv = 1.f / (float)hw;
+  float mu[8], rs[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float a = s1[e], b = s2[e];
+    for (int off = tpp; off < 64; off <<= 1) {
+      a += __shfl_xor(a, off, 64);
+      b += __shfl_xor(b, off, 64);
+    }
+    const float m1 = a * inv;
+    float var = b * inv - m1 * m1;
+    var = var > 0.f ? var : 0.f;
+    mu[e] = K[e] + m1;
+    rs[e] = rsqrtf(var + g.eps);
+  }
+  const __bf16* rb = res ? res + img * g.hw * g.c : nullptr;
+  __bf16* yb = y + img * g.hw * g.c;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int p = slot + k * ppw;
+    if (p >= hw) break;
+    float v[8], r[8];
+    unpack(raw[k], v);
+    if (rb) load8(rb + (int64_t)p * g.c + cg * 8, r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float o = (v[e] - mu[e]) * rs[e];
+      if (g.relu_inner) o = o > 0.f ? o : 0.f;
+      if (rb) o += r[e];
+      if (g.relu) o = o > 0.f ? o : 0.f;
+      v[e] = o;
+    }
+    store8(yb + (int64_t)p * g.c + cg * 8, v);
+  }
+}
+
 // chunks per image: ~1024 blocks over the launch, >= 4 pixel passes per block
 inline int in_chunks(int64_t n, int64_t hw, int64_t c) {
   const int64_t ppp = 256 / (c / 8);
@@ -698,6 +776,18 @@ extern "C" int comet_instnorm_nhwc(int dtype, const void* x, const void* res, vo
     int chunks = in_chunks(n, hw, c);
     if (chunks > 1 && (!workspace || workspace_bytes < n * chunks * 2 * c * (int64_t)sizeof(float))) chunks = 1;
     INGeo g{hw, cdiv(hw, chunks), (int)c, chunks, eps, relu, res_norm_relu};
+    // small bf16 images: one wave per image (in_wave_kernel)
+    const int tpp = (int)(c / 8), ppw = tpp > 0 && 64 % tpp == 0 ? 64 / tpp : 0;
+    const int64_t np = ppw ? cdiv(hw, ppw) : 0;
+    if (dtype == COMET_BF16 && chunks == 1 && ppw && np <= 16 && getenv("COMET_IN_NO_WAVE") == nullptr) {
+      const unsigned gw = (unsigned)cdiv(n, 4);
+      COMET_CHECK_ARG(cdiv(n, 4) < (1ll << 31), "comet_instnorm_nhwc: too many images");
+#define INW(NP) hipLaunchKernelGGL((in_wave_kernel<NP>), dim3(gw), dim3(256), 0, s, (const __bf16*)x, (const __bf16*)res, (__bf16*)y, n, g)
+      if (np <= 1) INW(1); else if (np <= 2) INW(2); else if (np <= 4) INW(4); else if (np <= 8) INW(8); else INW(16);
+#undef INW
+      COMET_CHECK_LAUNCH("comet_instnorm_nhwc (one wave per image)");
+      return COMET_OK;
+    }
 #define INL(T)                                                                                           \
   if (chunks == 1) {                                                                                     \
     COMET_CHECK_ARG(n <= 2147483647ll, "comet_instnorm_nhwc: too many images");                         \

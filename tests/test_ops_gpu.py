@@ -278,10 +278,12 @@ def test_instnorm_and_resize():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("n,c,h,w", [(2, 96, 128, 128), (700, 32, 16, 16), (3, 12, 9, 7), (5, 256, 33, 17), (1, 64, 8, 8)])
+@pytest.mark.parametrize("n,c,h,w", [(2, 96, 128, 128), (700, 32, 16, 16), (3, 12, 9, 7), (5, 256, 33, 17), (1, 64, 8, 8),
+                                     (999, 32, 4, 4), (333, 16, 8, 8), (17, 8, 5, 7), (9, 64, 12, 11)])
 @pytest.mark.parametrize("mode", ["plain", "inner_res_relu"])
 def test_instnorm_shapes(dtype, n, c, h, w, mode):
-    """Chunked (partials + apply), fused (one block per image) and generic (c % 8 != 0) paths;
+    """Chunked (partials + apply), fused (one block per image), one-wave-per-image (small bf16
+    images, incl. a partial last workgroup and partial pixel slots) and generic (c % 8 != 0) paths;
     inputs with a large common offset exercise the shifted-moment variance."""
     ops = _ops()
     x = (_rand(n, c, h, w, seed=30) * 0.5 + 40.0).to(dtype)
