@@ -106,8 +106,8 @@ __device__ __forceinline__ void write_tile(const f32x4 (&acc)[4][4], const Epi& 
 // (bf16) or 32-B (f32) vectors instead of 2-4-B column-strided scalars.
 constexpr int CP = 132;  // f32 pitch of the parked tile: conflict-free fragment writes
 
-template <typename TC, bool SPLIT>
-__device__ __forceinline__ void write_tile_lds(const f32x4 (&acc)[4][4], float* __restrict__ cs,
+template <typename TC, bool SPLIT, int MI = 4>
+__device__ __forceinline__ void write_tile_lds(const f32x4 (&acc)[MI][4], float* __restrict__ cs,
                                                const Epi& epi, TC* __restrict__ C, int64_t ldc,
                                                int64_t b0, int64_t b1, int64_t bz, int64_t m0, int64_t n0,
                                                int64_t M, int64_t N, const Split& sp, int wm, int wn, int lane) {
@@ -115,9 +115,9 @@ __device__ __forceinline__ void write_tile_lds(const f32x4 (&acc)[4][4], float* 
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cs[(wm * 64 + i * 16 + rq + r) * CP + wn * 64 + j * 16 + cl] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) cs[(wm * 16 * MI + i * 16 + rq + r) * CP + wn * 64 + j * 16 + cl] = acc[i][j][r];
   __syncthreads();
   const int t = threadIdx.x, cg = t & 15, rb = t >> 4;
   const int64_t col0 = n0 + cg * 8;
@@ -342,7 +342,9 @@ __device__ __forceinline__ bf16x8 frag(const __bf16* __restrict__ img, int rbase
   }
 }
 
-template <typename TC, int LA, int LB, int KA, int KB, bool SPLIT, bool CONV = false>
+// N64: outputs with N <= 64 (the 64-channel convolutions): the 4 waves split the 128 rows
+// (32 x 64 wave tiles) instead of a 2 x 2 grid whose right half would multiply zero columns.
+template <typename TC, int LA, int LB, int KA, int KB, bool SPLIT, bool CONV = false, bool N64 = false>
 __global__ void __launch_bounds__(NT, 2)
 gemm_bf16_kernel(const void* __restrict__ A, int64_t lda, int64_t sa0, int64_t sa1,
                  const void* __restrict__ B, int64_t ldb, int64_t sb0, int64_t sb1,
@@ -365,11 +367,13 @@ gemm_bf16_kernel(const void* __restrict__ A, int64_t lda, int64_t sa0, int64_t s
   }
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = N64 ? wid : wid >> 1, wn = N64 ? 0 : wid & 1;
+  constexpr int MI = N64 ? 2 : 4;  // 16-row fragments per wave (N64: 32-row wave tiles)
+  constexpr int WR = 16 * MI;
 
-  f32x4 acc[4][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -404,21 +408,21 @@ gemm_bf16_kernel(const void* __restrict__ A, int64_t lda, int64_t sa0, int64_t s
     const __bf16* Bs = smem[cur][1];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 a[4], b[4];
+      bf16x8 a[MI], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = frag<LA>(As, wm * 64 + i * 16, s, lane);
+      for (int i = 0; i < MI; ++i) a[i] = frag<LA>(As, wm * WR + i * 16, s, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) b[j] = frag<LB>(Bs, wn * 64 + j * 16, s, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
   }
-  write_tile_lds<TC, SPLIT>(acc, reinterpret_cast<float*>(&smem[0][0][0]), epi, C, ldc, b0, b1, bz, m0, n0, M, N, sp,
-                            wm, wn, lane);
+  write_tile_lds<TC, SPLIT, MI>(acc, reinterpret_cast<float*>(&smem[0][0][0]), epi, C, ldc, b0, b1, bz, m0, n0, M, N,
+                                sp, wm, wn, lane);
 }
 }  // namespace bf
 
@@ -2068,10 +2072,16 @@ int launch_conv(const comet_conv_args& a, hipStream_t s) {
       (a.resid == nullptr || ((uintptr_t)a.resid % (4 * sizeof(TC)) == 0 && a.ldr % 4 == 0)))
     return launch_conv_skinny<TC>(a, M, (int)oh, (int)ow, (int)K, s);
   Split sp{nullptr, K};
-  hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, 0, 0, bf::K_BF16_VEC, bf::K_BF16_VEC, false, true>),
-                     dim3((unsigned)(tiles_m * tiles_n), 1, 1), dim3(NT), 0, s,
-                     nullptr, 0, 0, 0, reinterpret_cast<const __bf16*>(a.weight), a.ldw, 0, 0,
-                     reinterpret_cast<TC*>(a.y), a.ldy, 0, 0, M, N, K, 1, (int)tiles_n, e, sp, g);
+  if (N <= 64 && getenv("COMET_CONV_NO_N64") == nullptr)  // 4 x 1 waves over 128 x 64: no zero columns
+    hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, 0, 0, bf::K_BF16_VEC, bf::K_BF16_VEC, false, true, true>),
+                       dim3((unsigned)(tiles_m * tiles_n), 1, 1), dim3(NT), 0, s,
+                       nullptr, 0, 0, 0, reinterpret_cast<const __bf16*>(a.weight), a.ldw, 0, 0,
+                       reinterpret_cast<TC*>(a.y), a.ldy, 0, 0, M, N, K, 1, (int)tiles_n, e, sp, g);
+  else
+    hipLaunchKernelGGL((bf::gemm_bf16_kernel<TC, 0, 0, bf::K_BF16_VEC, bf::K_BF16_VEC, false, true>),
+                       dim3((unsigned)(tiles_m * tiles_n), 1, 1), dim3(NT), 0, s,
+                       nullptr, 0, 0, 0, reinterpret_cast<const __bf16*>(a.weight), a.ldw, 0, 0,
+                       reinterpret_cast<TC*>(a.y), a.ldy, 0, 0, M, N, K, 1, (int)tiles_n, e, sp, g);
   COMET_CHECK_LAUNCH("comet_conv2d_nhwc");
   return COMET_OK;
 }

@@ -100,7 +100,9 @@ def test_gemm_splitk_epilogue_batched(dtype):
                                  (1, 12, 12, 416, 256, 3, 1, 1), (2, 20, 18, 8, 64, 7, 2, 3), (65, 9, 9, 32, 32, 3, 2, 1),
                                  # narrow-output path (M >= 16384, cout <= 64)
                                  (200, 16, 16, 32, 32, 3, 1, 1), (100, 31, 31, 8, 32, 3, 2, 1), (64, 20, 20, 16, 64, 3, 1, 1),
-                                 (300, 16, 16, 32, 32, 1, 2, 0), (70, 30, 30, 8, 48, 3, 1, 1)])
+                                 (300, 16, 16, 32, 32, 1, 2, 0), (70, 30, 30, 8, 48, 3, 1, 1),
+                                 # 128 x 64 (N <= 64) tile: the BasicEncoder's 64 -> 64 convolutions
+                                 (4, 40, 40, 64, 64, 3, 1, 1), (3, 21, 19, 64, 56, 3, 1, 1)])
 @pytest.mark.parametrize("epi", ["bias", "bias_relu_resid"])
 def test_conv2d_nhwc_implicit_gemm(geo, epi):
     """comet_conv2d_nhwc (implicit GEMM, bf16) vs torch conv2d in f64 on the same bf16 inputs."""
