@@ -1652,6 +1652,10 @@ int big_bn(const comet_gemm_args& a) {
   if ((a.layout_a == 1 && a.m % 8 != 0) || (a.layout_b == 1 && a.n % 8 != 0)) return 0;
   if (!wide && a.m < 4096) return 0;
   if (a.m < 256 || a.n < 128) return 0;
+  // short-K weight gradients over few 256-row tiles (M = N = 768, K = 128 tokens: 9 workgroups)
+  // run faster as 36 128 x 128 tiles
+  if (wide && a.k < 16 * 64 && cdiv(a.m, 256) * cdiv(a.n, 256) * 4 <= 256 && getenv("COMET_GEMM_NO_SMALLSPLIT") == nullptr)
+    return 0;
   const int64_t w256 = cdiv(a.n, 256) * 256 - a.n, w128 = cdiv(a.n, 128) * 128 - a.n;
   if (a.n >= 512 && w256 * 100 <= 15 * a.n) return 256;
   if (a.n % 256 == 0 || (a.n >= 512 && w128 * 100 <= 15 * a.n)) return 128;  // N = 384: 128 x 128 measured faster
@@ -1729,7 +1733,17 @@ int choose_splits(const comet_gemm_args& a) {
   const int64_t tiles = cdiv(a.m, BM) * cdiv(a.n, BN) * a.batch[0] * a.batch[1];
   const int bk = a.dtype_ab == COMET_BF16 ? bf::BK : f32::BK;
   const int64_t ktiles = cdiv(a.k, bk);
-  if (tiles >= kCUs || ktiles < 16) return 1;
+  if (tiles >= kCUs || ktiles < 16) {
+    // few tiles over a short K (the camera trunk's M = 128 token GEMMs: 6 tiles ran 12 serial
+    // k-tiles each on 6 CUs): split while every split keeps >= 2 k-tiles (bf16 operands only)
+    if (a.dtype_ab == COMET_BF16 && tiles * 4 <= kCUs && ktiles >= 4 && getenv("COMET_GEMM_NO_SMALLSPLIT") == nullptr) {
+      int64_t s = cdiv(2 * kCUs, tiles);
+      if (s > ktiles / 2) s = ktiles / 2;
+      if (s > 64) s = 64;
+      return s < 1 ? 1 : (int)s;
+    }
+    return 1;
+  }
   int64_t s = cdiv(2 * kCUs, tiles);
   const int64_t smax = ktiles / 8;
   if (s > smax) s = smax;
