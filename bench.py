@@ -5,6 +5,11 @@ sequences/s of train_e2epose2.py fwd+bwd bf16, B=8 per GPU, T=16, 512x512, N=512
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`--gpus N` without a launcher (WORLD_SIZE unset): this process runs the CPU baseline, then spawns
+N fresh worker processes (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, nothing on
+the GPU touched here first) and exits with their status; fewer than N visible devices is an error,
+never a silent 1-GPU run. Under torch.distributed.run, WORLD_SIZE must equal --gpus.
+
 One step = full COMET forward (coarse + fine tracker, DINOv2, camera head; tracker/backbone
 frozen under no_grad as in the reference) + pose loss + backward through the camera head + RCCL
 gradient all-reduce (N > 1) + clip_grad_norm_(1.0) + AdamW + LR schedule. Inputs are synthetic
@@ -40,8 +45,80 @@ def parse():
                     help="BASELINE configs[1]: full COMET forward only (eval, no_grad), no loss backward / optimizer")
     ap.add_argument("--cpu-baseline-only", action="store_true")
     ap.add_argument("--cpu-baseline-full", action="store_true",
-                    help="with --cpu-baseline-only: every SURVEY 8(d) mode (train/eval x fp32/bf16), 2 reps each")
+                    help="every SURVEY 8(d) CPU mode (train/eval x fp32/bf16), 2 reps each (default line: train fp32 only)")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="CPU self-test of the --gpus N launcher: gloo ranks, one bucketed gradient all-reduce, no GPU")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """One fresh process per GPU (the driver's `--gpus N` without torch.distributed.run). The
+    children re-run this script with the rank environment a launcher would set; rank 0 prints the
+    JSON line. Any failing rank stops the others; the exit status is the first failure's."""
+    import subprocess
+    port = free_port()
+    env = dict(os.environ)
+    env.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                "COMET_BENCH_SPAWNED": "1"})
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=e))
+    rc = 0
+    alive = set(range(n))
+    while alive:
+        for r in list(alive):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            alive.discard(r)
+            if c != 0 and rc == 0:
+                rc = c
+                print(f"[bench] rank {r} exited with {c}; stopping the other ranks", file=sys.stderr, flush=True)
+                for o in alive:
+                    procs[o].terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def launcher_check(rank, world):
+    """--launcher-check worker: gloo process group on CPU, a small model's gradients through
+    comet_amd.ddp.GradBucketer (two steps: discovery + rebuilt buckets), checked against the mean
+    of every rank's local gradient."""
+    import torch.distributed as dist
+    from comet_amd.ddp import GradBucketer
+    dist.init_process_group("gloo")
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.ReLU(), torch.nn.Linear(64, 8))
+    bk = GradBucketer(net.parameters(), bucket_mb=0.004)
+    ok = True
+    for step in range(2):
+        xs = [torch.randn(4, 16, generator=torch.Generator().manual_seed(10 * step + r)) for r in range(world)]
+        ref = [torch.zeros_like(p) for p in net.parameters()]
+        for x in xs:  # expected: mean of the per-rank gradients
+            g = torch.autograd.grad(net(x).square().mean(), list(net.parameters()))
+            for a, b in zip(ref, g):
+                a += b / world
+        bk.prepare_backward()
+        net(xs[rank]).square().mean().backward()
+        bk.finish_backward()
+        ok &= all(torch.allclose(p.grad, e, rtol=1e-5, atol=1e-7) for p, e in zip(net.parameters(), ref))
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print(json.dumps({"launcher_check": True, "n_gpus": dist.get_world_size(), "backend": dist.get_backend(),
+                          "buckets": len(bk.buckets), "reduced": bool(flag.item())}), flush=True)
+    dist.destroy_process_group()
+    return 0 if flag.item() else 1
 
 
 def synthetic(B, T, S_img, N, device, seed):
@@ -166,18 +243,33 @@ def pmc_traffic(instance, config):
 
 def main():
     args = parse()
+    cpu_modes = tuple(CPU_MODES) if args.cpu_baseline_full else ("train_fp32",)
+    cpu_reps = 2 if args.cpu_baseline_full else 1
+    if args.cpu_baseline_only:
+        print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks, modes=cpu_modes, reps=cpu_reps)))
+        return 0
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        # this process spawns the ranks; it never touches the GPU (device_count does not
+        # initialise HIP on this image), so the children start on a clean device
+        if not args.launcher_check:
+            have = torch.cuda.device_count()
+            if have < args.gpus:
+                print(f"[bench] --gpus {args.gpus} but only {have} GPU(s) visible; refusing to report a "
+                      f"{have}-GPU run as {args.gpus}", file=sys.stderr, flush=True)
+                return 2
+        return spawn_ranks(args.gpus)  # (the CPU baseline leg is an N = 1 figure only)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.cpu_baseline_only:
-        if args.cpu_baseline_full:
-            print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks, modes=tuple(CPU_MODES), reps=2)))
-        else:
-            print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks)))
-        return
+    if launched and world != args.gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        return 2
+    if args.launcher_check:
+        return launcher_check(rank, world)
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.frames, args.image, args.tracks)
+    if world == 1 and not args.no_cpu_baseline:  # rank 0 at N = 1 only
+        cpu = cpu_baseline(args.frames, args.image, args.tracks, modes=cpu_modes, reps=cpu_reps)
         torch.set_num_threads(max(1, min(8, os.cpu_count() or 1)))
 
     import torch.distributed as dist
@@ -241,6 +333,30 @@ def main():
 
     elapsed, loss = timed(False)          # value: plain timed region
     elapsed_prof, _ = timed(True)         # same K steps with per-launch HIP events
+    comm = None
+    if world > 1:
+        # the step's gradient exchange alone: every bucket all-reduced back to back (the in-step
+        # all-reduces overlap the backward, so this is an upper bound of what they add)
+        nbytes = sum(f.numel() * f.element_size() for f in ddp.flat)
+        reps = 5
+        dist.barrier()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            works = [dist.all_reduce(f, op=dist.ReduceOp.AVG, async_op=True) for f in ddp.flat]
+            for w in works:
+                w.wait()
+        e1.record()
+        torch.cuda.synchronize()
+        t = torch.tensor([e0.elapsed_time(e1) / reps], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = t.item()
+        comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "buckets": len(ddp.flat),
+                "bytes_per_step": nbytes, "allreduce_ms_per_step_isolated": round(ms, 3),
+                "algbw_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                "busbw_GBps": round(2 * (world - 1) / world * nbytes / (ms * 1e-3) / 1e9, 1),
+                "share_of_step": round(ms / (elapsed / args.steps * 1e3), 4)}
     prof_i = PROF.summary(instances=True)
     prof = {}
     for k, v in prof_i.items():
@@ -278,14 +394,14 @@ def main():
         out = {
             "metric": ("sequences/sec (BxT frames) COMET fwd-only" if fwd else "sequences/sec (BxT frames) COMET fwd+bwd")
                       + f", T={T} {args.image}^2",
-            "value": round(value, 4), "unit": "sequences/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 4), "unit": "sequences/s", "n_gpus": dist.get_world_size() if world > 1 else 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) frames, U[0,511] tracks, random unit quaternions); random-init weights",
             "config": {"workload": ("COMET fwd-only eval (BASELINE configs[1]): tracker+DINOv2+head, pose loss, no backward" if fwd else
                                     "train_e2epose2.py fwd+bwd (BASELINE configs[2]): COMET tracker+DINOv2+head, loss, backward, "
                                     "grad all-reduce, clip 1.0, AdamW"), "global_batch": B * world, "seq_len": T,
                        "image": args.image, "tracks": args.tracks, "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu, "kernels": kernels, "kernel_instances": instances, "final_loss": float(loss.item()) if loss is not None else None,
+            "roofline": roof, "cpu_baseline": cpu, "distributed": comm, "kernels": kernels, "kernel_instances": instances, "final_loss": float(loss.item()) if loss is not None else None,
             "ms_per_step_profiled": round(elapsed_prof / args.steps * 1e3, 2),
             "algorithmic_tflop_per_seq": tflop_seq if (T == 16 and args.image == 512) else None,
             "model_tflops": round(tflop_seq * value, 2) if (T == 16 and args.image == 512) else None,
@@ -296,4 +412,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

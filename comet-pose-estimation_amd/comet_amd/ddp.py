@@ -16,6 +16,8 @@ Bucket layout (what torch DDP does with find_unused_parameters + bucket rebuildi
     never-executed params (FeatureFusion, motion encoders, ...) are excluded, so no bucket waits
     on a gradient that never comes: each bucket's all-reduce starts during the backward.
     Excluded params keep .grad = None, so AdamW skips them as torch does.
+Buckets launch in index order (a completed bucket waits for the lower ones), as torch's Reducer
+does, so every rank issues the same sequence of collectives.
 `static_used` (the params that receive gradients, in bucket order) skips discovery when the set is
 known up front.
 """
@@ -63,8 +65,20 @@ class GradBucketer:
     def _rebuild_from_arrival(self):
         idx = torch.tensor([self.index[p] for p in self.arrival], dtype=torch.int64)
         if self.world > 1:
-            n = torch.tensor([idx.numel()], dtype=torch.int64)
             dev = self.flat[0].device if self.backend == "nccl" else torch.device("cpu")
+            # every rank must have used the same set of params: MIN and MAX of the per-param
+            # 'used' mask over ranks agree only then; all ranks see the same verdict and raise
+            # together (instead of one rank raising next step while the others block in all_reduce)
+            used = torch.zeros(len(self.params), dtype=torch.int32)
+            used[idx] = 1
+            lo, hi = used.to(dev), used.to(dev).clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+            if not torch.equal(lo.cpu(), hi.cpu()):
+                diff = (lo != hi).nonzero().flatten().tolist()
+                raise RuntimeError(f"GradBucketer: ranks used different parameter sets in the discovery step "
+                                   f"(param indices {diff[:8]}{'...' if len(diff) > 8 else ''})")
+            n = torch.tensor([idx.numel()], dtype=torch.int64)
             n = n.to(dev)
             dist.broadcast(n, 0, group=self.group)
             buf = torch.zeros(int(n.item()), dtype=torch.int64, device=dev)
@@ -94,6 +108,7 @@ class GradBucketer:
             p.grad = self._view(p) if p in self.slot else None
         self.pending = [len(pl) for pl in self.buckets]
         self.launched = [False] * len(self.buckets)
+        self.next_launch = 0  # buckets launch in index order on every rank (RCCL needs one order)
         self.works = []
         self.arrived = set()
         self.arrival = []
@@ -120,13 +135,18 @@ class GradBucketer:
                                "has one (the graph changed); build the bucketer with static_used")
         bi = self.slot[p][0]
         self.pending[bi] -= 1
-        if self.pending[bi] == 0 and not self.discovering:
-            self._launch(bi)
+        if not self.discovering:
+            # like torch's Reducer: a completed bucket waits for every lower-index bucket, so all
+            # ranks issue their collectives in the same order whatever order the grads arrive in
+            while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
+                self._launch(self.next_launch)
+                self.next_launch += 1
 
     def finish_backward(self):
         self.in_backward = False
         for bi in range(len(self.buckets)):
             self._launch(bi)
+        self.next_launch = len(self.buckets)
         for bi, w in self.works:
             w.wait()
             if self.backend != "nccl":

@@ -131,12 +131,23 @@ def _free_port():
     return port
 
 
-def _inputs():
+SIZES = {  # name -> (seed, T, image, N, dtype)
+    "golden": (31, 4, 128, 16, torch.float32),
+    # the headline per-sequence workload (BASELINE configs[3] is configs[2] per rank): T=16, 512^2,
+    # N=512, bf16 -- 2 ranks x B=1 against the single-process B=2
+    "headline": (37, 16, 512, 512, torch.bfloat16),
+}
+SELECT = ("fc_depth.weight", "trunk.3.mlp.fc2.weight", "pose_token", "self_att.0.attn.in_proj_weight",
+          "cross_att.3.mlp.fc1.weight", "traj_encoder.mlp.3.weight")
+
+
+def _inputs(size):
     from oracle import prng
-    return prng.synthetic_batch(31, 2, 4, 128, 128, 16)
+    seed, T, S, N, _ = SIZES[size]
+    return prng.synthetic_batch(seed, 2, T, S, S, N)
 
 
-def _rank(rank, world, port, q, paths):
+def _rank(rank, world, port, q, paths, size):
     import sys
     sys.path[:0] = paths
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -146,66 +157,95 @@ def _rank(rank, world, port, q, paths):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from comet_amd import functional as F
         from comet_amd.ddp import GradBucketer
-        from comet_amd.train import build_optimizer
         model, cfg = _model()
+        T, dtype = SIZES[size][1], SIZES[size][4]
+        img, tracks, gt = _inputs(size)
+        img, tracks, cams = img[rank:rank + 1].cuda(), tracks[rank:rank + 1].cuda(), _cams(_sub(gt, rank, T))
+
+        def fwd_bwd():
+            with F.precision(dtype):
+                out = model(img, gt_cameras=cams, training=True, tracks=tracks)
+                out["loss"].backward()
+        # this rank's own (local, un-reduced) gradients first
+        fwd_bwd()
+        torch.cuda.synchronize()
+        local = {k: p.grad.detach().cpu().numpy().copy() for k, p in model.camera_predictor.named_parameters()
+                 if p.grad is not None and k in SELECT}
+        model.zero_grad(set_to_none=True)
         bk = GradBucketer(model.camera_predictor.parameters(), bucket_mb=25)
-        img, tracks, gt = _inputs()
         res = []
         for step in range(2):  # step 0 = bucket discovery, step 1 = rebuilt buckets with overlap
-            with F.precision(torch.float32):
-                out = model(img[rank:rank + 1].cuda(), gt_cameras=_cams(_sub(gt, rank, 4)), training=True,
-                            tracks=tracks[rank:rank + 1].cuda())
-                model.zero_grad(set_to_none=True)
-                bk.prepare_backward()
-                out["loss"].backward()
-                bk.finish_backward()
+            model.zero_grad(set_to_none=True)
+            bk.prepare_backward()
+            fwd_bwd()
+            bk.finish_backward()
             torch.cuda.synchronize()
             res.append({k: p.grad.double().norm().item() for k, p in model.camera_predictor.named_parameters()
                         if p.grad is not None})
             # numpy, not torch tensors: a torch CPU tensor crosses the queue as a shared-memory file
             # descriptor that vanishes when this process exits before the parent reads it
             g = {k: p.grad.detach().cpu().numpy().copy() for k, p in model.camera_predictor.named_parameters()
-                 if p.grad is not None and k in ("fc_depth.weight", "trunk.3.mlp.fc2.weight", "pose_token")}
+                 if p.grad is not None and k in SELECT}
         during = all(d for _, d in bk.launch_log)
-        q.put((rank, res, g, during, len(bk.buckets)))
+        q.put((rank, res, g, during, len(bk.buckets), local))
         dist.destroy_process_group()
     except Exception as e:  # surface the error to the parent
         import traceback
-        q.put((rank, None, traceback.format_exc(), None, None))
+        q.put((rank, None, traceback.format_exc(), None, None, None))
         raise
 
 
-def test_ddp_simulated_ranks_equal_B2_gradients():
+@pytest.mark.parametrize("size", ["golden", "headline"])
+def test_ddp_simulated_ranks_equal_B2_gradients(size):
+    """Every rank's all-reduced gradient (a) equals the mean of the two ranks' local gradients
+    (exact up to summation order: the exchange itself), and (b) equals the single-process B=2
+    gradient (batch independence of the model: fp32 1e-4; bf16 within the bf16 tolerance, as B=2
+    and B=1 take different GEMM tilings)."""
     from comet_amd import functional as F
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, [ROOT, PKG])) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, q, [ROOT, PKG], size)) for r in range(2)]
     for p in procs:
         p.start()
     got = {}
     for _ in range(2):
-        rank, res, g, during, nb = q.get(timeout=300)
+        rank, res, g, during, nb, local = q.get(timeout=600)
         assert res is not None, g
-        got[rank] = (res, g, during, nb)
+        got[rank] = (res, g, during, nb, local)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # single process, B = 2
+    # (a) the exchange: reduced == mean of the local gradients
+    for rank in (0, 1):
+        for k, v in got[rank][1].items():
+            mean = (got[0][4][k].astype(np.float64) + got[1][4][k].astype(np.float64)) / 2
+            err = np.abs(v - mean).max() / max(np.abs(mean).max(), 1e-30)
+            print(f"{size} rank {rank} {k}: reduced vs mean(local) rel-to-max {err:.2e}")
+            assert err < 1e-5, (rank, k, err)
+    # (b) single process, B = 2
+    seed, T, S, N, dtype = SIZES[size]
     model, cfg = _model()
-    img, tracks, gt = _inputs()
-    with F.precision(torch.float32):
+    img, tracks, gt = _inputs(size)
+    with F.precision(dtype):
         out = model(img.cuda(), gt_cameras=_cams(gt), training=True, tracks=tracks.cuda())
         out["loss"].backward()
     torch.cuda.synchronize()
     ref = {k: p.grad for k, p in model.camera_predictor.named_parameters() if p.grad is not None}
+    norm_tol, elem_tol = (1e-4, 1e-4) if dtype == torch.float32 else (2e-2, 3e-2)
+    worst = 0.0
     for rank in (0, 1):
-        res, g, during, nb = got[rank]
+        res, g, during, nb, _ = got[rank]
         assert during and nb > 1, "rebuilt buckets must all launch during the backward"
         for step in (0, 1):
             assert set(res[step]) == set(ref)
             for k, n in res[step].items():
                 r = ref[k].double().norm().item()
-                assert abs(n - r) <= 1e-4 * r + 1e-7, (rank, step, k, n, r)
+                worst = max(worst, abs(n - r) / max(r, 1e-12))
+                assert abs(n - r) <= norm_tol * r + 1e-7, (rank, step, k, n, r)
         for k, v in g.items():
-            torch.testing.assert_close(torch.from_numpy(v), ref[k].cpu(), rtol=1e-4, atol=1e-4 * ref[k].abs().max().item())
+            e = (torch.from_numpy(v).double() - ref[k].cpu().double()).abs().max().item()
+            rel = e / ref[k].abs().max().item()
+            print(f"{size} rank {rank} {k}: DDP vs B=2 rel-to-max {rel:.2e}")
+            assert rel < elem_tol, (rank, k, rel)
+    print(f"{size}: worst gradient-norm relative difference DDP vs B=2 {worst:.2e}")
