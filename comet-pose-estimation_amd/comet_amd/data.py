@@ -13,6 +13,13 @@ comet_lanczos_crop_resize (libcomet_hip.so) crops, LANCZOS-resizes (byte-exact w
 Resample.c) and ImageNet-normalises all T frames into the model's [T, 3, H, W] float32 input on
 the device, instead of T PIL crops + resizes + a float normalisation on the CPU
 (kubric_movif_SFM_dataset_YT.py:236-260). Decoding stays with PIL (the reference's decoder).
+
+Two stages, so the dataset sits behind forked DataLoader workers as the reference's does
+(num_workers 8, train_util.py:829-840): `__getitem__` is host-only (decode, masks, GT, crop box;
+returns the uint8 `frames` [T, H, W, 3] and `crop_box` instead of `images`), `collate_host` batches
+such samples, and the device stage (`to_device` / `DeviceLoader`, in the main process) uploads the
+frames and produces `images` [B, T, 3, h, w]. `load_images_from_folder` is both stages in one call
+(the reference's per-sequence function, for in-process use).
 """
 import ctypes
 import os
@@ -150,8 +157,9 @@ def crop_resize_normalize(frames, box, crop_size, mean=IMAGENET_MEAN, std=IMAGEN
 
 
 class YTDataset(torch.utils.data.Dataset):
-    """kubric_movif_SFM_dataset_YT.py:94-300 (same constructor and sample dict); `images` is produced
-    on `device` by crop_resize_normalize."""
+    """kubric_movif_SFM_dataset_YT.py:94-300 (same constructor and sample fields). Indexing is
+    host-only (worker-safe); `images` is produced on `device` by load_images_from_folder or, for
+    DataLoader batches, by to_device / DeviceLoader in the main process."""
 
     def __init__(self, data_root, crop_size=(256, 256), seq_len=24, use_augs=False, split="train", device="cuda"):
         super().__init__()
@@ -238,4 +246,56 @@ class YTDataset(torch.utils.data.Dataset):
         return len(self.seq_names)
 
     def __getitem__(self, index):
-        return self.load_images_from_folder(self.seq_names[index])
+        """Host stage only (no HIP call: safe in forked workers): the sample dict with `frames`
+        (uint8 [T, H, W, 3]) and `crop_box` (int64 [4]) in place of `images`."""
+        frames, square, meta = self.load_host(self.seq_names[index])
+        meta["frames"] = torch.from_numpy(np.stack(frames, 0))
+        meta["crop_box"] = torch.tensor(square, dtype=torch.int64)
+        meta["crop_size"] = torch.tensor([int(self.crop_size[0]), int(self.crop_size[1])], dtype=torch.int64)
+        return meta
+
+
+def collate_host(samples):
+    """DataLoader collate_fn for YTDataset samples (runs in the workers): `frames` stay a list
+    (sequences may differ in frame size), every other field through default_collate."""
+    from torch.utils.data import default_collate
+    frames = [s["frames"] for s in samples]
+    rest = default_collate([{k: v for k, v in s.items() if k != "frames"} for s in samples])
+    rest["frames"] = frames
+    return rest
+
+
+def to_device(batch, device="cuda", keep_frames=False):
+    """Device stage of a collate_host batch (main process): uploads each sequence's frames and
+    crops / LANCZOS-resizes / normalises them -> batch["images"] [B, T, 3, h, w] f32 on `device`
+    (the reference loader's collated `images`)."""
+    dev = torch.device(device)
+    imgs = []
+    for b, fr in enumerate(batch["frames"]):
+        up = fr.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" and not fr.is_cuda else fr.to(dev)
+        box = [int(v) for v in batch["crop_box"][b]]
+        size = [int(v) for v in batch["crop_size"][b]]
+        imgs.append(crop_resize_normalize(up, box, size))
+    out = dict(batch)
+    out["images"] = torch.stack(imgs, 0)
+    if not keep_frames:
+        out.pop("frames")
+    return out
+
+
+class DeviceLoader:
+    """Wraps a DataLoader of collate_host batches and applies to_device in the consuming process,
+    so the workers never touch the GPU; len() and iteration as the wrapped loader's."""
+
+    def __init__(self, loader, device="cuda"):
+        self.loader, self.device = loader, device
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        for batch in self.loader:
+            yield to_device(batch, self.device)
+
+    def __getattr__(self, k):
+        return getattr(self.loader, k)

@@ -1,0 +1,485 @@
+"""Loop-side callers of the COMET path (SURVEY §8(c) "Build counterpart of Python callers").
+
+  process_spark_data2  train_util.py:637-667: batch dict -> (images, T_xyz, T_uvz, R, fl, pp, ratio,
+                       seq_name, image_names, first_mask, R_matrix) on the device; default focal
+                       cfg.default_focal_length and principal point (W/2, H/2) when absent
+  train_or_eval_fn     train_eval_func_new_cp5.py:514-823, train and eval branches: keypoint
+                       tracks from frame 0 (track_by_spsg: SuperPoint, comet_amd.keypoints; SIFT is
+                       not available), QuaternionCameras from the batch (597-606),
+                       model(..., training) (under no_grad for eval), loss.mean(), the eval block's
+                       pose metrics (comet_amd.metrics.pose_metrics), Stats, then for training
+                       zero_grad -> accelerator.backward -> clip_grad_norm_ -> optimizer.step ->
+                       lr_scheduler.step
+  Stats                the subset of pytorch3d.implicitron Stats / train_util.VizStats the loop and
+                       train_fn use (update / new_epoch / get_epoch_averages / status string /
+                       gzip-JSON save and load); pytorch3d is not a dependency of this build
+  CometAccelerator     the subset of accelerate.Accelerator train_e2epose2.py uses, on this build's
+                       pieces: one process per GPU (RCCL), prepare() shards the train loader's
+                       batches over ranks and attaches comet_amd.ddp.GradBucketer, backward() runs
+                       the bucketed all-reduce, clip_grad_norm_ defers the scaling into the fused
+                       AdamW kernel, mixed_precision "bf16" runs the model under
+                       functional.precision(bf16), save_state / load_state write / read accelerate's
+                       checkpoint files (comet_amd.checkpoint)
+  build_dataset        train_util.py:335-347 for "AMD" / "AMD_eval": YTDataset behind DataLoaders
+                       with the reference's loader settings, host stage in the workers and the
+                       crop / resize on the device in this process (DeviceLoader)
+  train_fn             train_e2epose2.py:45-186
+"""
+import gzip
+import json
+import os
+import random
+import time
+from contextlib import nullcontext
+
+import numpy as np
+import torch
+
+from . import checkpoint as ckpt
+from . import functional as F
+from .models.utils import QuaternionCameras
+
+TO_PLOT_METRICS = ("lr", "Auc_30", "Auc_10", "Auc_5", "Auc_3", "X_err", "Y_err", "Z_err", "Tx_mse", "Ty_mse",
+                   "Tz_mse", "T_avg", "Racc_him_5", "Racc_him_10", "Racc_him_15", "R_avg", "Tacc_him_5",
+                   "Tacc_him_10", "Tacc_him_15", "acc@5deg_x", "acc@5deg_y", "acc@5deg_z", "sec/it")  # train_util.py:96-121
+
+
+def _get(cfg, path, default):
+    cur = cfg
+    for p in path.split("."):
+        if isinstance(cur, dict) and p in cur:
+            cur = cur[p]
+        else:
+            return default
+    return cur
+
+
+def process_spark_data2(batch, device, cfg):
+    """train_util.py:637-667 (the `"spark" or ...` condition there is always true)."""
+    images = batch["images"].to(device)
+    translation = batch["T"].to(device)
+    T_uvz = batch["T_uvz"].to(device) if "T_uvz" in batch else None
+    rotation = batch["R"].to(device)
+    ratio = batch["ratio"].to(device) if "ratio" in batch else None
+    names = batch.get("seq_name")
+    first_mask = batch.get("first_mask")
+    image_names = batch.get("image_names")
+    R_matrix_gt = batch.get("R_matrix")
+    B, S = images.shape[:2]
+    if "fl" in batch:
+        fl = batch["fl"].to(device)
+    else:
+        fl = torch.ones(B, S, 2, device=device) * _get(cfg, "default_focal_length", 1745)
+    if "pp" in batch:
+        pp = batch["pp"].to(device)
+    else:
+        H, W = images.shape[-2:]
+        pp = torch.tensor([W / 2, H / 2], device=device).expand(B, S, 2)
+    return images, translation, T_uvz, rotation, fl, pp, ratio, names, image_names, first_mask, R_matrix_gt
+
+
+# ------------------------------------------------------------------------------------------------
+class AverageMeter:
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.val, self.sum, self.count, self.history = 0.0, 0.0, 0, []
+
+    def update(self, val, n=1, epoch=0):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+
+    @property
+    def avg(self):
+        return self.sum / max(self.count, 1)
+
+    def get_epoch_averages(self):
+        return self.history
+
+
+class Stats:
+    """Per stat_set ("train" / "eval") running averages of `log_vars` over the current epoch
+    (pytorch3d.implicitron.tools.stats.Stats semantics: `sec/it` = wall time since time_start over
+    iterations; tensors are averaged to Python floats)."""
+
+    def __init__(self, log_vars, epoch=-1):
+        self.log_vars = list(log_vars)
+        self.epoch = epoch
+        self.it = {}
+        self.stats = {}
+
+    def hard_reset(self, epoch=-1):
+        self.epoch = epoch
+        self.it, self.stats = {}, {}
+
+    def new_epoch(self):
+        self.epoch += 1
+        self.it, self.stats = {}, {}
+
+    def update(self, preds, time_start=None, stat_set="train", freeze_iter=False):
+        it = self.it.get(stat_set, -1) + (0 if freeze_iter else 1)
+        self.it[stat_set] = it
+        meters = self.stats.setdefault(stat_set, {})
+        for k in self.log_vars:
+            if k == "sec/it":
+                if time_start is None:
+                    continue
+                v = (time.time() - time_start) / (it + 1)
+                meters.setdefault(k, AverageMeter()).reset()
+            elif k in preds and preds[k] is not None:
+                v = preds[k]
+            else:
+                continue
+            if torch.is_tensor(v):
+                v = float(v.detach().float().mean())
+            meters.setdefault(k, AverageMeter()).update(float(v))
+
+    def get_epoch_averages(self):
+        out = {}
+        for ss, meters in self.stats.items():
+            d = {k: m.avg for k, m in meters.items()}
+            d["epoch"] = self.epoch
+            d["it"] = self.it.get(ss, -1)
+            out[ss] = d
+        return out
+
+    def get_status_string(self, stat_set="train", max_it=None):
+        it = self.it.get(stat_set, -1)
+        head = f"{stat_set} | epoch {self.epoch:3d} | it {it:5d}" + (f"/{max_it:5d}" if max_it else "")
+        body = " | ".join(f"{k}: {m.avg:.4f}" for k, m in self.stats.get(stat_set, {}).items())
+        return head + (" | " + body if body else "")
+
+    def to_json(self):
+        return json.dumps({"log_vars": self.log_vars, "epoch": self.epoch, "it": self.it,
+                           "stats": {ss: {k: [m.val, m.sum, m.count] for k, m in ms.items()}
+                                     for ss, ms in self.stats.items()}})
+
+    def save(self, flpath):
+        flpath = flpath if flpath.endswith(".jgz") else flpath + ".jgz"
+        with gzip.open(flpath, "wt", encoding="utf-8") as f:
+            f.write(self.to_json())
+
+    @staticmethod
+    def load(flpath):
+        flpath = flpath if flpath.endswith(".jgz") else flpath + ".jgz"
+        with gzip.open(flpath, "rt", encoding="utf-8") as f:
+            d = json.loads(f.read())
+        self = Stats(d["log_vars"], d["epoch"])
+        self.it = d["it"]
+        for ss, ms in d["stats"].items():
+            for k, (val, sm, cnt) in ms.items():
+                m = self.stats.setdefault(ss, {}).setdefault(k, AverageMeter())
+                m.val, m.sum, m.count = val, sm, cnt
+        return self
+
+
+# ------------------------------------------------------------------------------------------------
+class _BatchShard(torch.utils.data.Sampler):
+    """Batch i of the wrapped batch sampler goes to rank i % world (accelerate's default batch
+    dispatch, split_batches=False); the tail that does not fill every rank is dropped so all
+    ranks run the same number of steps."""
+
+    def __init__(self, batch_sampler, rank, world):
+        self.bs, self.rank, self.world = batch_sampler, rank, world
+
+    def __len__(self):
+        return len(self.bs) // self.world
+
+    def __iter__(self):
+        n = len(self)
+        for i, b in enumerate(self.bs):
+            if i // self.world >= n:
+                break
+            if i % self.world == self.rank:
+                yield b
+
+
+class CometAccelerator:
+    def __init__(self, mixed_precision="no", device=None, bucket_mb=25):
+        import torch.distributed as dist
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        if device is None:
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            device = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+        self.device = torch.device(device)
+        self.mixed_precision = mixed_precision
+        self.bucket_mb = bucket_mb
+        self.ddp = None
+        self._optimizer = None
+        self.step = 0
+
+    @property
+    def is_main_process(self):
+        return self.rank == 0
+
+    @property
+    def num_processes(self):
+        return self.world
+
+    def print(self, *a, **k):
+        if self.is_main_process:
+            print(*a, **k)
+
+    def autocast(self):
+        if self.mixed_precision == "bf16":
+            return F.precision(torch.bfloat16)
+        if self.mixed_precision == "fp16":
+            raise ValueError("mixed_precision fp16 is not supported by this build (the reference config uses bf16)")
+        return nullcontext()
+
+    def _shard(self, dl):
+        if self.world == 1 or dl is None or getattr(dl, "batch_sampler", None) is None:
+            return dl
+        from .data import DeviceLoader
+        inner = dl.loader if isinstance(dl, DeviceLoader) else dl
+        kw = dict(batch_sampler=_BatchShard(inner.batch_sampler, self.rank, self.world), num_workers=inner.num_workers,
+                  collate_fn=inner.collate_fn, pin_memory=inner.pin_memory, worker_init_fn=inner.worker_init_fn,
+                  generator=inner.generator)
+        if inner.num_workers > 0:
+            kw.update(prefetch_factor=inner.prefetch_factor, persistent_workers=inner.persistent_workers)
+        out = torch.utils.data.DataLoader(inner.dataset, **kw)
+        return DeviceLoader(out, dl.device) if isinstance(dl, DeviceLoader) else out
+
+    def prepare(self, model, dataloader=None, optimizer=None, lr_scheduler=None):
+        """accelerator.prepare(model, dataloader, optimizer, lr_scheduler) (train_e2epose2.py:83):
+        model to the device, train loader sharded over ranks, gradient buckets over the
+        optimizer's params (the camera predictor) when world > 1. The optimizer's own clip is
+        switched off: the loop clips through clip_grad_norm_ as the reference does."""
+        model = model.to(self.device)
+        if optimizer is not None and hasattr(optimizer, "max_norm"):
+            optimizer.max_norm = None
+        self._optimizer = optimizer
+        if self.world > 1 and optimizer is not None:
+            from .ddp import GradBucketer
+            params = [p for g in optimizer.param_groups for p in g["params"]]
+            self.ddp = GradBucketer(params, bucket_mb=self.bucket_mb)
+        return model, self._shard(dataloader), optimizer, lr_scheduler
+
+    def backward(self, loss):
+        if self.ddp is not None:
+            self.ddp.prepare_backward()
+        loss.backward()
+        if self.ddp is not None:
+            self.ddp.finish_backward()
+
+    def clip_grad_norm_(self, parameters, max_norm, optimizer=None):
+        """-> total norm before clipping (device scalar). With a CometAdamW the scaling is applied
+        by its next step(); otherwise torch.nn.utils.clip_grad_norm_."""
+        opt = optimizer if optimizer is not None else getattr(self, "_optimizer", None)
+        if opt is not None and hasattr(opt, "clip_grad_norm_"):
+            return opt.clip_grad_norm_(max_norm)
+        return torch.nn.utils.clip_grad_norm_(list(parameters), max_norm)
+
+    def save_state(self, output_dir, model, optimizer=None, lr_scheduler=None, safe_serialization=False):
+        if safe_serialization:
+            raise ValueError("safe_serialization=True is not used by the reference (train_e2epose2.py:160)")
+        return ckpt.save_state(output_dir, model, optimizer, lr_scheduler, step=self.step, process_index=self.rank)
+
+    def load_state(self, input_dir, model, optimizer=None, lr_scheduler=None):
+        self.step = ckpt.load_state(input_dir, model, optimizer, lr_scheduler, process_index=self.rank,
+                                    device=self.device)
+
+
+# ------------------------------------------------------------------------------------------------
+def _keypoint_init(cfg, device):
+    from .keypoints import SuperPoint
+    return SuperPoint(max_num_keypoints=_get(cfg, "train.track_num", 512), detection_threshold=0.005).to(device).eval()
+
+
+def train_or_eval_fn(model, dataloader, cfg, optimizer, stats, accelerator, lr_scheduler, training=True, epoch=-1,
+                     sp=None):
+    """train_eval_func_new_cp5.py:514-823 (visualisation / demo-JSON branches excluded).
+    `sp`: a SuperPoint detector to reuse across calls (built here when track_by_spsg is set)."""
+    model.train() if training else model.eval()
+    time_start = time.time()
+    max_it = len(dataloader)
+    dev = accelerator.device
+    spsg = bool(_get(cfg, "enable_track", True) and _get(cfg, "track_by_spsg", False)
+                and not _get(cfg, "labor_input_traj", False))
+    if spsg and sp is None:
+        sp = _keypoint_init(cfg, dev)
+    acc5 = [0.0, 0.0, 0.0]
+    for step, batch in enumerate(dataloader):
+        (images, T_xyz, T_uvz, rotation, fl, pp, ratio, sel_first_name, image_names, mask,
+         R_matrix_gt) = process_spark_data2(batch, dev, cfg)
+        bbb, ttt = images.shape[:2]
+        if spsg:
+            from .keypoints import keypoint_tracks
+            tracks, tracks_visibility = keypoint_tracks(sp, images, mask.to(dev).bool(), _get(cfg, "train.track_num", 512),
+                                                        sift=None, min_required=256, names=sel_first_name)
+        else:
+            tracks, tracks_visibility = None, None
+        gt_cameras = None
+        if rotation is not None:
+            gt_cameras = QuaternionCameras(focal_length=fl.reshape(-1, 2), principal_point=pp.reshape(-1, 2),
+                                           R=rotation.reshape(-1, 4), T_uvz=T_uvz.reshape(-1, 3),
+                                           T=T_xyz.reshape(-1, 3), ratio=ratio, device=dev)
+        with accelerator.autocast():
+            if training:
+                predictions = model(images, gt_cameras=gt_cameras, training=True, tracks=tracks,
+                                    tracks_visibility=tracks_visibility)
+                predictions["loss"] = predictions["loss"].mean()
+                loss = predictions["loss"]
+            else:
+                with torch.no_grad():
+                    predictions = model(images, gt_cameras=gt_cameras, training=False, tracks=tracks,
+                                        tracks_visibility=tracks_visibility)
+                predictions["loss"] = predictions["loss"].mean()
+        if "gt_pose_enc" in predictions and predictions["gt_pose_enc"] is not None:
+            from .metrics import pose_metrics
+            with torch.no_grad():
+                predictions.update(pose_metrics(predictions, gt_cameras, bbb, dev))
+            for i, k in enumerate(("acc@5deg_x", "acc@5deg_y", "acc@5deg_z")):
+                acc5[i] += float(predictions[k])
+        ss = "train" if training else "eval"
+        stats.update(predictions, time_start=time_start, stat_set=ss)
+        pi = _get(cfg, "train.print_interval" if training else "train.eval_print_interval", 50)
+        if pi and step % pi == 0:
+            accelerator.print(stats.get_status_string(stat_set=ss, max_it=max_it))
+        if training:
+            optimizer.zero_grad()
+            accelerator.backward(loss)
+            clip = _get(cfg, "train.clip_grad", 1.0)
+            if clip > 0:
+                accelerator.clip_grad_norm_(model.parameters(), clip, optimizer=optimizer)
+            optimizer.step()
+            lr_scheduler.step()
+            accelerator.step += 1
+    n = max(len(dataloader), 1)
+    accelerator.print("x", "y", "z", acc5[0] / n, acc5[1] / n, acc5[2] / n)
+    return True
+
+
+# ------------------------------------------------------------------------------------------------
+def seed_worker(worker_id):
+    """train_util.py:803-806."""
+    s = torch.initial_seed() % 2 ** 32
+    np.random.seed(s)
+    random.seed(s)
+
+
+def set_seed_and_print(seed, device_specific=True):
+    """train_util.py:1847-1849 (accelerate.utils.set_seed(seed, device_specific=True): seed +
+    process index for python, numpy and torch)."""
+    import torch.distributed as dist
+    if device_specific and dist.is_initialized():
+        seed += dist.get_rank()
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    print(f"----------Seed is set to {np.random.get_state()[1][0]} now----------")
+
+
+def build_dataset(cfg, data_root=None, device="cuda"):
+    """train_util.py:335-347, 808-926 for the YT datasets ("AMD": train + eval loaders,
+    "AMD_eval": eval loader only). data_root: the directory holding AMD_train / AMD_eval
+    (the reference's comet/datasets/AMD; cfg.data_root or $COMET_DATA_ROOT here)."""
+    from torch.utils.data import ConcatDataset, DataLoader, SequentialSampler
+    from .data import DeviceLoader, YTDataset, collate_host
+    name = _get(cfg, "train.dataset", "AMD")
+    if name not in ("AMD", "AMD_eval"):
+        raise ValueError("Dataset Not Implemented")
+    root = data_root or _get(cfg, "data_root", None) or os.environ.get("COMET_DATA_ROOT")
+    if root is None:
+        raise ValueError("build_dataset: give data_root (the reference's comet/datasets/AMD directory)")
+    size = int(_get(cfg, "train.img_size", 512))
+    nw = int(_get(cfg, "train.num_workers", 8))
+    mk = lambda split, augs: YTDataset(os.path.join(root, "AMD_train" if split == "train" else "AMD_eval"),  # noqa: E731
+                                       crop_size=[size, size], seq_len=int(_get(cfg, "seqlen", 16)), use_augs=augs,
+                                       split=split, device=device)
+    eval_dataset = mk("valid", False)
+    eval_loader = DeviceLoader(DataLoader(eval_dataset, sampler=SequentialSampler(eval_dataset), batch_size=1,
+                                          num_workers=nw, pin_memory=True, persistent_workers=nw > 0,
+                                          collate_fn=collate_host), device)
+    if name == "AMD_eval":
+        return None, None, None, eval_loader
+    train_dataset = ConcatDataset([mk("train", True)] * int(_get(cfg, "repeat_kub", 1)))
+    g = torch.Generator()
+    g.manual_seed(0)
+    kw = dict(prefetch_factor=1) if nw > 0 else {}
+    train_loader = DeviceLoader(DataLoader(train_dataset, batch_size=int(_get(cfg, "batch_size", 1)), shuffle=True,
+                                           persistent_workers=False, num_workers=nw, worker_init_fn=seed_worker,
+                                           generator=g, pin_memory=True, drop_last=True, collate_fn=collate_host, **kw),
+                                device)
+    return train_dataset, eval_dataset, train_loader, eval_loader
+
+
+def train_fn(cfg, data_root=None, eval_only=True, csv_log=True):
+    """train_e2epose2.py:45-186. As written, the reference returns right after the first
+    evaluation (train_e2epose2.py:131, `return` before the epoch loop); `eval_only=True` keeps that
+    behaviour, `eval_only=False` runs the epoch loop that follows it (train, ckpt_DDDDDD every
+    ckpt_interval epochs, eval every eval_interval epochs, a final checkpoint)."""
+    from .config import instantiate
+    from .train import build_optimizer
+    acc = CometAccelerator(mixed_precision=_get(cfg, "mixed_precision", "no"))
+    set_seed_and_print(int(_get(cfg, "seed", 0)))
+    exp_dir = _get(cfg, "exp_dir", "exp")
+    logger = None
+    if acc.is_main_process and csv_log:
+        import csv
+        os.makedirs(exp_dir, exist_ok=True)
+        path = os.path.join(exp_dir, "train_eval_stats.csv")
+        fields = ["epoch", "it", "mode"] + list(TO_PLOT_METRICS) + ["lr"]
+        if not os.path.exists(path):
+            with open(path, "w", newline="") as f:
+                csv.DictWriter(f, fieldnames=fields).writeheader()
+
+        def logger(row):
+            with open(path, "a", newline="") as f:
+                csv.DictWriter(f, fieldnames=fields).writerow(row)
+    dataset, eval_dataset, dataloader, eval_dataloader = build_dataset(cfg, data_root, acc.device)
+    model = instantiate(cfg["MODEL"], _recursive_=False, cfg=cfg).to(acc.device)
+    optimizer, lr_scheduler = build_optimizer(cfg, model, dataloader if dataloader is not None else 1)
+    resume = _get(cfg, "train.resume_ckpt", "")
+    if resume:
+        acc.print(f"Loading ckpt from {resume}")
+        model = ckpt.load_model_weights(model, resume, acc.device, _get(cfg, "relax_load", False))
+    model, dataloader, optimizer, lr_scheduler = acc.prepare(model, dataloader, optimizer, lr_scheduler)
+    start_epoch = 0
+    stats = Stats(TO_PLOT_METRICS)
+    if _get(cfg, "train.auto_resume", False):
+        last = ckpt.find_last_checkpoint(exp_dir)
+        ep, start = ckpt.resume_epoch(last)
+        if last is not None and ep > 0:
+            acc.print(f"Loading ckpt from {last}")
+            acc.load_state(last, model, optimizer, lr_scheduler)
+            start_epoch = start
+            try:
+                stats = Stats.load(os.path.join(last, "train_stats.jgz"))
+            except (OSError, ValueError, KeyError):
+                stats.hard_reset(epoch=start_epoch)
+
+    def run_eval(epoch):
+        lr = lr_scheduler.get_last_lr()[0]
+        train_or_eval_fn(model, eval_dataloader, cfg, optimizer, stats, acc, lr_scheduler, training=False, epoch=epoch)
+        stats.update({"lr": lr}, stat_set="eval")
+        d = stats.get_epoch_averages()["eval"]
+        if logger:
+            logger({"epoch": d["epoch"], "it": d["it"], "mode": "eval", **{k: d.get(k, "") for k in TO_PLOT_METRICS}})
+
+    run_eval(start_epoch - 1)
+    if eval_only:
+        return
+    epoch = start_epoch
+    for epoch in range(start_epoch, int(_get(cfg, "train.epochs", 1))):
+        stats.new_epoch()
+        set_seed_and_print(int(_get(cfg, "seed", 0)) + epoch * 1000)
+        train_or_eval_fn(model, dataloader, cfg, optimizer, stats, acc, lr_scheduler, training=True, epoch=epoch)
+        if acc.is_main_process:
+            stats.update({"lr": lr_scheduler.get_last_lr()[0]}, stat_set="train")
+            d = stats.get_epoch_averages()["train"]
+            if logger:
+                logger({"epoch": d["epoch"], "it": d["it"], "mode": "train", "lr": d.get("lr", ""),
+                        **{k: d.get(k, "") for k in TO_PLOT_METRICS if k != "lr"}})
+        if epoch != 0 and epoch % int(_get(cfg, "train.ckpt_interval", 1)) == 0 and acc.is_main_process:
+            path = ckpt.checkpoint_path(exp_dir, epoch)
+            acc.save_state(path, model, optimizer, lr_scheduler)
+            ckpt.save_tdict(path, epoch, cfg)
+            stats.save(os.path.join(path, "train_stats.jgz"))
+        if epoch != 0 and epoch % int(_get(cfg, "train.eval_interval", 1)) == 0:
+            run_eval(epoch)
+    acc.save_state(ckpt.checkpoint_path(exp_dir, epoch), model, optimizer, lr_scheduler)
+    return True

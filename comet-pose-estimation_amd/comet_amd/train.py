@@ -62,6 +62,15 @@ class CometAdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.max_norm = max_norm
         self.last_sqnorm = None
+        self._pending = None  # (max_norm, squared norm) from clip_grad_norm_, used by the next step
+
+    def clip_grad_norm_(self, max_norm):
+        """accelerator.clip_grad_norm_(params, max_norm) of the reference loop
+        (train_eval_func_new_cp5.py:797): the total gradient norm now (device scalar, no sync);
+        the scaling itself is applied inside the next step()'s AdamW kernel."""
+        sq = self.grad_sqnorm()
+        self._pending = (float(max_norm), sq)
+        return sq.sqrt()
 
     @property
     def lr(self):
@@ -75,8 +84,34 @@ class CometAdamW(torch.optim.Optimizer):
     def _with_grad(self):
         return [p for g in self.param_groups for p in g["params"] if p.grad is not None]
 
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict, then every per-param `step` as a host float32
+        scalar: a capturable / fused AdamW checkpoint keeps it on the device, and reading it there
+        would cost one device sync per param and step."""
+        super().load_state_dict(state_dict)
+        for st in self.state.values():
+            s = st.get("step")
+            if torch.is_tensor(s) and (s.device.type != "cpu" or s.dtype != torch.float32):
+                st["step"] = s.detach().to("cpu", torch.float32)
+
+    @staticmethod
+    def _check(p, st):
+        """comet_adamw_multi takes raw f32 pointers: param, grad and both moments must be
+        contiguous f32 tensors on the param's device, or the kernel would stride wrongly."""
+        ts = (p, p.grad, st["exp_avg"], st["exp_avg_sq"])
+        for t in ts:
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != p.device or t.shape != p.shape:
+                raise L.CometHipError(f"CometAdamW: param / grad / moments must be contiguous float32 of the param's "
+                                      f"shape on {p.device}; got {t.dtype} {tuple(t.shape)} on {t.device} "
+                                      f"(contiguous={t.is_contiguous()})")
+
     def grad_sqnorm(self, ps=None):
         ps = ps if ps is not None else self._with_grad()
+        for p in ps:
+            g = p.grad
+            if g.dtype != torch.float32 or not g.is_contiguous() or g.device != ps[0].device:
+                raise L.CometHipError(f"CometAdamW: gradients must be contiguous float32 on {ps[0].device}; got "
+                                      f"{g.dtype} on {g.device} (contiguous={g.is_contiguous()})")
         out = torch.zeros(1, device=ps[0].device, dtype=torch.float32)
         arr = (ctypes.c_void_p * len(ps))(*[p.grad.data_ptr() for p in ps])
         sz = (ctypes.c_int64 * len(ps))(*[p.numel() for p in ps])
@@ -94,9 +129,15 @@ class CometAdamW(torch.optim.Optimizer):
         ps = self._with_grad()
         if not ps:
             return loss
-        max_norm = max_norm if max_norm is not None else self.max_norm
+        pend, self._pending = self._pending, None
+        if max_norm is None and pend is not None:
+            max_norm, sq = pend
+        else:
+            max_norm = max_norm if max_norm is not None else self.max_norm
+            sq = None
         clip = max_norm is not None and max_norm > 0
-        sq = self.grad_sqnorm(ps) if clip else None
+        if clip and sq is None:
+            sq = self.grad_sqnorm(ps)
         for g in self.param_groups:
             # params of one launch share lr / betas / step count (torch keeps `step` per param;
             # params that skipped earlier steps form their own launch)
@@ -109,7 +150,8 @@ class CometAdamW(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
+                self._check(p, st)
+                st["step"] += 1  # a host scalar (load_state_dict keeps it there): no device sync
                 by_step.setdefault(int(st["step"].item()), []).append(p)
             b1, b2 = g["betas"]
             for step, plist in by_step.items():

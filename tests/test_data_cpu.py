@@ -116,3 +116,26 @@ def test_ytdataset_host_part_matches_reference(tag, dataset_root):
     video = torch.from_numpy(imgs).permute(0, 3, 1, 2).float() / 255.0
     video = (video - torch.from_numpy(MEAN)[None, :, None, None]) / torch.from_numpy(STD)[None, :, None, None]
     np.testing.assert_array_equal(video.numpy(), g[pre + "images"])
+
+
+def test_ytdataset_behind_forked_dataloader_workers(dataset_root):
+    """The reference loads with DataLoader(num_workers=8) (train_util.py:829-840): __getitem__ is
+    host-only, so forked workers work; each worker's sample equals the in-process host stage.
+    seq_len = the sequence length (12 frames) makes the frame choice RNG-free (start 0, stride 1)."""
+    from torch.utils.data import DataLoader
+    from comet_amd.data import YTDataset, collate_host
+    ds = YTDataset(dataset_root, crop_size=(64, 48), seq_len=12, device="cpu")
+    dl = DataLoader(ds, batch_size=2, num_workers=2, collate_fn=collate_host,
+                    multiprocessing_context="fork")
+    batches = list(dl)
+    assert len(batches) == 1
+    b = batches[0]
+    assert len(b["frames"]) == 2 and "images" not in b
+    for i, name in enumerate(ds.seq_names):
+        frames, square, meta = ds.load_host(name)
+        assert torch.equal(b["frames"][i], torch.from_numpy(np.stack(frames, 0)))
+        assert b["crop_box"][i].tolist() == list(square)
+        assert b["seq_name"][i] == name
+        for k in ("T", "R", "T_uvz", "first_mask"):
+            assert torch.equal(b[k][i], meta[k]), k
+        assert float(b["ratio"][i]) == meta["ratio"]

@@ -60,3 +60,21 @@ def test_ytdataset_on_device_matches_reference(tag, dataset_root):
     for k in ("T", "R", "T_uvz"):
         np.testing.assert_array_equal(smp[k].numpy(), g[pre + k], err_msg=k)
     assert smp["ratio"] == float(g[pre + "ratio"][0])
+
+
+def test_device_loader_after_cuda_init_with_forked_workers(dataset_root):
+    """with HIP already initialised in the parent, forked DataLoader workers must not
+    touch the GPU. The host stage runs in the workers, DeviceLoader's device stage in this process;
+    the images equal the in-process load_images_from_folder bit for bit."""
+    from torch.utils.data import DataLoader
+    from comet_amd.data import DeviceLoader, YTDataset, collate_host
+    torch.zeros(1, device="cuda")  # HIP initialised before the workers fork
+    ds = YTDataset(dataset_root, crop_size=(64, 48), seq_len=12)
+    dl = DeviceLoader(DataLoader(ds, batch_size=2, num_workers=2, collate_fn=collate_host,
+                                 multiprocessing_context="fork"), "cuda")
+    assert len(dl) == 1
+    (b,) = list(dl)
+    assert b["images"].is_cuda and tuple(b["images"].shape) == (2, 12, 3, 48, 64)
+    for i, name in enumerate(ds.seq_names):
+        ref = ds.load_images_from_folder(name)
+        assert torch.equal(b["images"][i], ref["images"])
