@@ -169,3 +169,64 @@ def test_headline_bf16_end_to_end_B2(setup, gold):
         print(f"sequence {b}: max |ours - reference bf16| {np.abs(e).max():.3e}")
         assert (np.abs(e) <= 1e-2 + slack).all(), f"sequence {b}: bf16 vs reference bf16 beyond 1e-2 + its own slack"
     close(out["loss"].reshape(1), gold["head_bf16_loss"], 2e-2, 1e-2, "loss (bf16)")
+
+
+def test_headline_bf16_camera_head_fwd_bwd(setup, gold):
+    """The product's training precision (bf16 operands, f32 accumulation / residual stream) through
+    the camera head's forward AND backward at the headline size, on the reference's own stage
+    inputs, against the reference's bf16-autocast head fwd+bwd (tools/gen_golden.py
+    --headline-bf16-head). This runs the kernels the bench times for the backward: the bf16 flash
+    attention backward (dK/dV and dQ kernels, D=96), the 256-row split-K / ragged-K weight-gradient
+    GEMMs (K = 16 x 577 tokens), the bf16 LayerNorm backward and the activation-gradient column sums.
+
+    Tolerance: a bf16 gradient is compared with the reference's bf16 gradient allowing 2e-2 of the
+    fp32 value plus twice the reference's own bf16 deviation at that element (|ref_bf16 - ref_fp32|):
+    some head gradients (fc_depth, confidence_attention) move by O(1) relative between the
+    reference's own fp32 and bf16 runs, so two correct bf16 implementations may differ by that much.
+    Pose encoding: 1e-2 against the reference fp32 (north-star tolerance) and within 1e-2 + the
+    reference's bf16 deviation against its bf16 output, as the forward test."""
+    from comet_amd import functional as F
+    model, cfg, img, tracks, gt = setup
+    cp = model.camera_predictor
+    B = img.shape[0]
+    refined = torch.from_numpy(gold["head_refined"]).cuda()
+    conf = torch.from_numpy(gold["head_pred_score"]).cuda()
+    model.zero_grad(set_to_none=True)
+    with F.precision(torch.bfloat16):
+        out = cp(img.reshape(-1, *img.shape[2:]), batch_size=B, gt_cameras=_cams(gt), iters=cfg["camera_iter"],
+                 pred_trajectories=refined, track_confidence=conf)
+        out["loss"].backward()
+    torch.cuda.synchronize()
+    enc = out["pred_pose_enc"].double().cpu().numpy()
+    ref16, ref32 = gold["head_bf16h_pred_pose_enc"], gold["head_pred_pose_enc"]
+    close(enc[:, :3], ref32[:, :3], 0, 1e-2, "uvz (bf16 head vs reference fp32)")
+    close(enc[:, 3:], ref32[:, 3:], 0, 1e-2, "quaternion (bf16 head vs reference fp32)")
+    e16 = np.abs(enc - ref16)
+    print(f"pose enc: max |ours - reference bf16| {e16.max():.3e}")
+    assert (e16 <= 1e-2 + np.abs(ref16 - ref32)).all()
+    close(out["loss"].reshape(1), gold["head_bf16h_loss"], 1e-2, 1e-3, "loss (bf16 head)")
+    named = dict(cp.named_parameters())
+    names = [str(k) for k in gold["head_grad_names"]]
+    assert all(named[k].grad is not None for k in names)
+    norms = np.array([named[k].grad.double().norm().item() for k in names])
+    n16, n32 = gold["head_bf16h_grad_norms"], gold["head_grad_norms"]
+    allow = 2e-2 * n32 + 2 * np.abs(n16 - n32) + 1e-6
+    err = np.abs(norms - n16)
+    tight = np.abs(n16 - n32) <= 1e-2 * n32
+    print(f"169 gradient norms: max rel err vs reference bf16 {np.max(err / n16):.3e}; "
+          f"{int(tight.sum())} params where the reference's bf16 is within 1e-2 of its fp32: max rel err there "
+          f"{np.max((err / n32)[tight]):.3e}")
+    bad = [(names[i], norms[i], n16[i], n32[i]) for i in np.nonzero(err > allow)[0]]
+    assert not bad, bad[:8]
+    for k in gold:
+        if k.startswith("head_bf16h_grad_full."):
+            name = k[len("head_bf16h_grad_full."):]
+            g16, g32 = gold[k], gold["head_fp32h_grad_full." + name]
+            got = named[name].grad.double().cpu().numpy().reshape(named[name].shape[0], -1)[:g16.shape[0]]
+            got = got.reshape(g16.shape)
+            scale = float(np.abs(g32).max())
+            d = np.abs(got - g16)
+            ok = d <= 2e-2 * scale + 2 * np.abs(g16 - g32)
+            print(f"{name}: max |ours - ref bf16| / max|ref| {d.max() / scale:.3e}")
+            assert ok.all(), f"{name}: {int((~ok).sum())} elements beyond tolerance"
+    model.zero_grad(set_to_none=True)

@@ -393,6 +393,75 @@ def gen_headline(out):
         E2E.refine_track = orig
 
 
+HEAD_BF16_FULL = ["fc_depth.weight", "fc_translation2d.weight", "pose_branch.fc2.weight", "trunk.3.mlp.fc2.bias",
+                  "confidence_attention.0.weight", "traj_encoder.mlp.0.weight", "pose_token",
+                  "trunk.0.attn.in_proj_weight", "cross_att.3.cross_attn.in_proj_weight", "self_att.0.mlp.fc1.weight"]
+
+
+def _rows(g, n=48):
+    """a gradient in full when small, else its first n rows (the fixture stays small)"""
+    return np32(g if g.numel() <= 65536 else g.reshape(g.shape[0], -1)[:n])
+
+
+def gen_headline_bf16_head(out):
+    """The product's training precision at the headline size: the reference camera head
+    (camera_predictor10.py:288-460) forward under torch.autocast(bfloat16) -- accelerate's
+    mixed_precision="bf16" wraps the forward only -- and the backward of its loss, on the
+    reference's own fp32 stage inputs stored by gen_headline (refined tracks, pred_score), PRNG
+    weights seed 0: pose enc, loss, the 169 gradient norms and selected full gradients."""
+    torch.manual_seed(0)
+    cfg = H.load_cfg()
+    model = H.build_reference_comet(cfg)
+    P, P_hf = reference_state(model, SEED_W)
+    model.load_state_dict(P_hf, strict=True)
+    del P, P_hf
+    QC = H.reference_module("train_eval_func_new_cp5").QuaternionCameras
+    q = CFG_HEAD
+    img, tracks, gt = prng.synthetic_batch(SEED_X, q["B"], q["T"], q["H"], q["W"], q["N"])
+    cams = QC(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+              principal_point=gt["principal_point"], ratio=gt["ratio"])
+    refined = torch.from_numpy(out["head_refined"])
+    conf = torch.from_numpy(out["head_pred_score"])
+    cp = model.camera_predictor
+    import time
+    t0 = time.time()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        pred = cp(img.reshape(-1, *img.shape[2:]), batch_size=q["B"], gt_cameras=cams, iters=cfg.camera_iter,
+                  pred_trajectories=refined, track_confidence=conf)
+    model.zero_grad()
+    pred["loss"].mean().float().backward()
+    print(f"reference bf16 camera head fwd+bwd at headline size: {time.time() - t0:.1f} s")
+    grads = {k: p.grad for k, p in cp.named_parameters() if p.grad is not None}
+    names = sorted(grads)
+    assert names == [str(k) for k in out["head_grad_names"]], "bf16 and fp32 runs must grade the same params"
+    out["head_bf16h_pred_pose_enc"] = np32(pred["pred_pose_enc"].float())
+    out["head_bf16h_loss"] = np32(pred["loss"].float().reshape(1))
+    out["head_bf16h_loss_trans"] = np32(pred["loss_trans"].float().reshape(1))
+    out["head_bf16h_loss_rot"] = np32(pred["loss_rot"].float().reshape(1))
+    out["head_bf16h_grad_norms"] = np.array([grads[k].double().norm().item() for k in names])
+    for k in HEAD_BF16_FULL:
+        out["head_bf16h_grad_full." + k] = _rows(grads[k])
+    # the same selection from an fp32 pass, so the test can bound the reference's own bf16 deviation
+    model.zero_grad()
+    pred32 = cp(img.reshape(-1, *img.shape[2:]), batch_size=q["B"], gt_cameras=cams, iters=cfg.camera_iter,
+                pred_trajectories=refined, track_confidence=conf)
+    pred32["loss"].mean().backward()
+    for k in HEAD_BF16_FULL:
+        out["head_fp32h_grad_full." + k] = _rows(cp.get_parameter(k).grad)
+
+
+def main_headline_bf16_head():
+    """Adds the head_bf16h_* arrays to the existing comet_golden_headline.npz (its fp32 stage
+    tensors are the inputs)."""
+    H.require_reference()
+    torch.set_num_threads(8)
+    path = os.path.join(OUT, "comet_golden_headline.npz")
+    out = dict(np.load(path, allow_pickle=False))
+    gen_headline_bf16_head(out)
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
 def main_headline():
     H.require_reference()
     torch.set_num_threads(8)
@@ -691,6 +760,8 @@ if __name__ == "__main__":
         main_keypoints()
     elif "--metrics" in sys.argv:
         main_metrics()
+    elif "--headline-bf16-head" in sys.argv:
+        main_headline_bf16_head()
     elif "--headline" in sys.argv:
         main_headline()
     else:
