@@ -41,14 +41,6 @@ class RowLNArgs(ctypes.Structure):
     ]
 
 
-class MlpArgs(ctypes.Structure):
-    _fields_ = [
-        ("x", c_vp), ("ldx", c_i64), ("w1", c_vp), ("b1", c_vp), ("w2", c_vp), ("b2", c_vp),
-        ("resid", c_vp), ("ldr", c_i64), ("c", c_vp), ("ldc", c_i64),
-        ("m", c_i64), ("c_dim", c_i32), ("hidden", c_i32),
-    ]
-
-
 class ConvArgs(ctypes.Structure):
     _fields_ = [
         ("dtype", c_i32), ("dtype_y", c_i32),
@@ -102,8 +94,6 @@ SIGNATURES = {
     "comet_gemm_plan": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_int32)]),
     "comet_gemm_rowln_ok": (_INT, [ctypes.POINTER(GemmArgs)]),
     "comet_gemm_rowln": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(RowLNArgs), c_vp]),
-    "comet_mlp_rowln_ok": (_INT, [c_i64, _INT, _INT]),
-    "comet_mlp_rowln": (_INT, [ctypes.POINTER(MlpArgs), ctypes.POINTER(RowLNArgs), c_vp]),
     "comet_conv2d_nhwc": (_INT, [ctypes.POINTER(ConvArgs), c_vp]),
     "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
                                    c_i64, _F, _INT, c_vp]),
@@ -128,7 +118,6 @@ SIGNATURES = {
     "comet_instnorm_workspace": (_INT, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "comet_instnorm_nhwc": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, _F, _INT, _INT, c_vp, c_i64, c_vp]),
     "comet_resize_bilinear": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, _INT, c_vp]),
-    "comet_resize_pool_nhwc": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "comet_resize_bilinear_nhwc_into": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
                                                _INT, c_vp]),
     "comet_act_fwd": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_vp]),

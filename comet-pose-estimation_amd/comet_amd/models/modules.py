@@ -8,7 +8,6 @@ backward run through comet_amd.functional (libcomet_hip.so). Residual streams ar
   CrossAttnBlock modules.py:298-344   same with ctx = LN_affine(ctx, eps 1e-5)
   ResidualBlock  modules.py:39-116    conv3x3-IN-ReLU x2 (+ 1x1 s2 downsample), NHWC
 """
-import os
 
 import torch
 import torch.nn as nn
@@ -99,21 +98,10 @@ def dual_ctx(cross_blk):
     return dict(raw=False, y16_eps=1e-6, z=(n.weight, n.bias, n.eps))
 
 
-# opt-in (COMET_FUSED_MLP=1): the fused fc1 -> GELU -> fc2 kernel keeps the hidden tile in LDS but
-# its 64-deep register-staged steps (0.2 us of MFMA each) cannot hide the L2 latency of the weight
-# tiles every 128-row block re-streams: 711 vs 300 us unfused at M = 65536 (profiles/r02_mlp)
-FUSED_MLP_MIN_ROWS = 16384
-
-
 def _mlp_pre(blk, a, o, x32, out):
     # x = x + out_proj(o); x = x + mlp(norm2(x)): norm2 is written by the out_proj epilogue
     h32, h16, _ = _res_ln(o, a.out_proj.weight, a.out_proj.bias, x32, raw=True, y16_eps=1e-6)
     m = blk.mlp
-    w1, w2 = F.wcast(m.fc1.weight), F.wcast(m.fc2.weight)
-    if (os.environ.get("COMET_FUSED_MLP") and h16.numel() // h16.shape[-1] >= FUSED_MLP_MIN_ROWS
-            and ops.mlp_rowln_ok(h16, w1, w2, h32)):
-        # fc1 -> GELU -> fc2 + residual + the consumers' LayerNorms in one kernel (hidden stays in LDS)
-        return ops.mlp_rowln(h16, w1, m.fc1.bias, w2, m.fc2.bias, h32, **out)
     hid = F.linear(h16, m.fc1.weight, m.fc1.bias, act=L.ACT_GELU)
     return _res_ln(hid, m.fc2.weight, m.fc2.bias, h32, **out)
 

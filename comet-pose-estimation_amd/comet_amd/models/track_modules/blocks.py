@@ -8,7 +8,6 @@ im2col + MFMA GEMM, InstanceNorm/ReLU/residual tails are fused kernels.
   ShallowEncoder blocks.py:114-196  fine patch feature net -> [n, 31, 31, 32]
   EfficientUpdateFormer blocks.py:205-348 (time / virtual-track space attention)
 """
-import os
 
 import torch
 import torch.nn as nn
@@ -103,11 +102,6 @@ class ShallowEncoder(nn.Module):
                      resid=x.reshape(-1, c), out_dtype=x.dtype).reshape(n, h, w, c)
         oh, ow = H // self.stride, W // self.stride
         if with_pool:
-            # opt-in (COMET_RESIZE_POOL=1): the fused up-sample + pool kernel measured 0.7 ms/step slower
-            # than the two passes it replaces (profiles/r02_glue/ab2.txt)
-            r = ops.resize_pool_nhwc(x, oh, ow) if os.environ.get("COMET_RESIZE_POOL") else None
-            if r is not None:
-                return r
             y = ops.resize_bilinear(x, oh, ow, nhwc=True)
             return y, ops.avgpool2_nhwc(y)
         return ops.resize_bilinear(x, oh, ow, nhwc=True)

@@ -119,8 +119,6 @@ def _plan_name(la, lb, cdt, odt, split):
         return f"big{bn}.L{la}{lb}.{out}"
     if kind == 3:  # persistent tile kernel: _PLAN[2] = tile rows
         return f"pp{_PLAN[2]}x{bn}.L{la}{lb}.{out}"
-    if kind == 4:  # two workgroups per CU (gemm_w2.hip): _PLAN[2] = tile rows
-        return f"w2_{_PLAN[2]}x{bn}.L{la}{lb}.{out}"
     return f"tile128.L{la}{lb}.{'bf16' if cdt == torch.bfloat16 else 'f32'}.{out}"
 
 
@@ -251,43 +249,6 @@ def _ln_args(c_shape, dev, raw, y16_eps, z):
         z16 = torch.empty(*c_shape, device=dev, dtype=torch.bfloat16)
         a.z16, a.ldz, a.zw, a.zb, a.eps_z = z16.data_ptr(), N, zw.data_ptr(), zb.data_ptr(), float(zeps)
     return a, y16, z16
-
-
-def mlp_rowln_ok(x, w1, w2, resid):
-    if x.dtype != torch.bfloat16 or w1.dtype != torch.bfloat16 or w2.dtype != torch.bfloat16:
-        return False
-    if resid is None or resid.dtype != torch.float32 or x.stride(-1) != 1 or not w1.is_contiguous() or not w2.is_contiguous():
-        return False
-    C, Hd = x.shape[-1], w1.shape[0]
-    M = x.numel() // C
-    return bool(L.load().comet_mlp_rowln_ok(M, C, Hd)) and w2.shape == (C, Hd)
-
-
-def mlp_rowln(x, w1, b1, w2, b2, resid, *, raw=True, y16_eps=None, z=None):
-    """resid + fc2(GELU(fc1(x))) with the row LayerNorms of linear_rowln, one kernel per 128 rows
-    (comet_mlp_rowln). Returns (c, y16, z16) as linear_rowln."""
-    _req_cuda(x, w1, b1, w2, b2, resid)
-    C, Hd = x.shape[-1], w1.shape[0]
-    x2 = x.reshape(-1, C)
-    r2 = resid.reshape(-1, C)
-    M = x2.shape[0]
-    c = torch.empty(*x.shape[:-1], C, device=x.device, dtype=torch.float32)
-    g = L.MlpArgs()
-    g.x, g.ldx = x2.data_ptr(), x2.stride(0)
-    g.w1, g.b1, g.w2, g.b2 = w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr()
-    g.resid, g.ldr = r2.data_ptr(), r2.stride(0)
-    g.c, g.ldc = c.data_ptr(), C
-    g.m, g.c_dim, g.hidden = M, C, Hd
-    a, y16, z16 = _ln_args(c.shape, x.device, raw, y16_eps, z)
-    e0 = PROF.start()
-    L.check(L.load().comet_mlp_rowln(ctypes.byref(g), ctypes.byref(a), stream()), "comet_mlp_rowln")
-    if e0 is not None:
-        name = "comet_mlp_rowln"
-        if PROF.detail:
-            name = f"mlp_rowln M{M} C{C} H{Hd} raw{int(raw)} y16{int(y16 is not None)} z16{int(z16 is not None)}"
-        io = 2 * M * C + 4 * C * Hd + 4 * M * C * 2 + 2 * M * C * ((y16 is not None) + (z16 is not None))
-        PROF.stop(e0, name, 4.0 * M * C * Hd, float(io))
-    return c, y16, z16
 
 
 # ------------------------------------------------------------------------------------------
@@ -560,25 +521,6 @@ def resize_bilinear(x, oh, ow, nhwc, out=None, add=False, out_dtype=None):
     L.check(L.load().comet_resize_bilinear(dt(xc), dt(out), int(nhwc), _p(xc), _p(out), n, c, h, w, oh, ow,
                                            int(add), stream()), "resize_bilinear")
     return out
-
-
-def resize_pool_nhwc(x, oh, ow):
-    """(resize_bilinear(x, oh, ow) NHWC, its 2x2 average pool) in one pass (comet_resize_pool_nhwc);
-    None when the images do not fit the one-workgroup-per-image kernel."""
-    n, h, w, c = x.shape
-    es = x.element_size()
-    if c % 8 or h * w * c * es > 32768:
-        return None
-    xc = x.contiguous()
-    y = torch.empty(n, oh, ow, c, device=x.device, dtype=x.dtype)
-    p = torch.empty(n, oh // 2, ow // 2, c, device=x.device, dtype=x.dtype)
-    e0 = PROF.start()
-    L.check(L.load().comet_resize_pool_nhwc(dt(xc), dt(y), _p(xc), _p(y), _p(p), n, c, h, w, oh, ow, stream()),
-            "resize_pool_nhwc")
-    if e0 is not None:
-        PROF.stop(e0, f"resize_pool [{n}x{h}x{w}x{c}]" if PROF.detail else "comet_resize_pool_nhwc", 0.0,
-                  float(es * (n * h * w * c + y.numel() + p.numel())))
-    return y, p
 
 
 def cast_multi_f32_bf16(srcs, dsts):

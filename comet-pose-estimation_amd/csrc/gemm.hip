@@ -29,8 +29,6 @@
 
 namespace comet {
 
-bool w2_ok(const comet_gemm_args& a);                      // gemm_w2.hip (opt-in: COMET_GEMM_W2)
-int launch_w2_any(const comet_gemm_args& a, hipStream_t s);  // gemm_w2.hip
 
 namespace {
 
@@ -1753,7 +1751,6 @@ int choose_splits(const comet_gemm_args& a) {
 
 Plan make_plan(const comet_gemm_args& a) {
   if (skinny_ok(a)) return Plan{0, 0, 1};
-  if (w2_ok(a)) return Plan{4, 128, 1, 256};
   if (pp_ok(a)) {
     int tbm, tbn;
     pp_tile(a, tbm, tbn);
@@ -2191,7 +2188,6 @@ extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   const Plan plan = make_plan(a);
   if (plan.kind == 0) return a.dtype_c == COMET_BF16 ? launch_skinny<__bf16>(a, s) : launch_skinny<float>(a, s);
   if (plan.kind == 3) return a.dtype_c == COMET_BF16 ? launch_pp<__bf16>(a, s) : launch_pp<float>(a, s);
-  if (plan.kind == 4) return launch_w2_any(a, s);
   if (plan.kind == 1 && plan.tail && a.workspace != nullptr && a.workspace_bytes >= plan_workspace(a, plan)) {
     // slot 0: the K % 64 remainder (128 x 128 kernel, plain f32 output); slots 1..: the 256-row
     // kernel's split partials over the 64-multiple part; one reduce applies the epilogue

@@ -106,21 +106,6 @@ typedef struct comet_rowln_args {
 int comet_gemm_rowln_ok(const comet_gemm_args* args);
 int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_args* ln, void* stream);
 
-/* Fused update-former MLP (Mlp fc1 -> GELU -> fc2 + residual, modules.py:119-154, 285-294,
- * 334-343) with the row-LN epilogue of comet_gemm_rowln: v = resid + fc2(GELU(fc1(x))) per row,
- * the [m, hidden] activation kept in LDS per 128-row block. x [m, c_dim] bf16 (ldx), w1 [hidden,
- * c_dim] bf16, w2 [c_dim, hidden] bf16 (dense), b1 / b2 / resid / c f32; outputs as
- * comet_rowln_args. Eligible (comet_mlp_rowln_ok): c_dim 256 or 384, hidden % 128 == 0. */
-typedef struct comet_mlp_args {
-  const void* x; int64_t ldx;
-  const void* w1; const float* b1;
-  const void* w2; const float* b2;
-  const float* resid; int64_t ldr;
-  float* c; int64_t ldc;
-  int64_t m; int32_t c_dim; int32_t hidden;
-} comet_mlp_args;
-int comet_mlp_rowln_ok(int64_t m, int c_dim, int hidden);
-int comet_mlp_rowln(const comet_mlp_args* args, const comet_rowln_args* ln, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM convolution on channels-last activations (nn.Conv2d of BasicEncoder /
@@ -290,11 +275,6 @@ int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, const void* x, 
 /* NHWC resize into a channel slice of a wider NHWC tensor (output pixel pitch ldy elements):
  * BasicEncoder's four up-sampled maps land directly in their torch.cat(dim=1) positions
  * (blocks.py:97-107), so the 416-channel concat is never copied. c, ldy % 8 == 0. */
-/* NHWC align_corners resize (as comet_resize_bilinear) that also writes the 2x2 average pool of its
- * output: ShallowEncoder's final up-sample + the fine pyramid's first level (blocks.py:199-202,
- * CorrBlock pyramid), one workgroup per image (input image <= 32 KiB of LDS), c % 8 == 0. */
-int comet_resize_pool_nhwc(int dtype_in, int dtype_out, const void* x, void* y, void* p, int64_t n, int64_t c,
-                           int64_t h, int64_t w, int64_t oh, int64_t ow, void* stream);
 int comet_resize_bilinear_nhwc_into(int dtype_in, int dtype_out, const void* x, void* y, int64_t n,
                                     int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
                                     int64_t ldy, int add, void* stream);

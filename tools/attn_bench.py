@@ -1,7 +1,6 @@
 """Microbenchmark of comet_attention_fwd / _bwd on the COMET step's attention shapes.
 
     python tools/attn_bench.py > gpurun_out/attn_bench.txt
-    COMET_ATTN_V2=1 python tools/attn_bench.py     # opt-in v2 forward kernel, for comparison
 
 TFLOP/s counts 4*B*H*Lq*Lk*D (forward) and 10*B*H*Lq*Lk*D (backward) at the true head_dim.
 """
