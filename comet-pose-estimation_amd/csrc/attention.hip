@@ -431,6 +431,202 @@ attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, i
   }
 }
 
+// bf16 forward on 32x32x16 MFMAs (D = 32, 48, 64, 96), one workgroup = 4 waves = 128 queries of one
+// (batch, head), 2 workgroups per CU. Per wave: 32 queries; per 64-key tile
+//  * Sᵀ = K·Qᵀ as two 32x32 blocks (keys x queries; D / 16 k-steps each, Q fragments in registers):
+//    a lane holds one query and 16 keys of each block, so the row max / sum are 32 lane-local values
+//    plus one v_permlane32_swap with the partner half;
+//  * P stays in the accumulator registers: registers 8s..8s+7 of a block, packed to bf16, are the
+//    B fragment of k-step s of Oᵀ = Vᵀ·Pᵀ, whose k order (16s + 8(j>>2) + 4h + (j&3)) the Vᵀ
+//    fragments follow: two ds_read_b64_tr_b16 of 4 consecutive keys each;
+//  * K / V tiles: global loads into registers issued before the tile's MFMAs, written to the other
+//    LDS buffer after them, one barrier per tile (rows padded by 16 B: conflict-free b128 and
+//    tr16 reads).
+// A 32x32x16 MFMA carries twice the work of a 16x16x32 one for the same 8 cycles of vector issue,
+// which the softmax (about 20 cycles of VALU per score per lane) needs.
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+attn_fwd32_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int64_t sq_l,
+                  const __bf16* __restrict__ K, int64_t sk_b, int64_t sk_h, int64_t sk_l,
+                  const __bf16* __restrict__ V, int64_t sv_b, int64_t sv_h, int64_t sv_l,
+                  __bf16* __restrict__ O, int64_t so_b, int64_t so_h, int64_t so_l,
+                  float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2, Inner in) {
+  static_assert(D % 16 == 0 && D <= 128, "D: multiple of 16");
+  constexpr int NKS = D / 16;            // k-steps of Sᵀ = K·Qᵀ
+  constexpr int DB = (D + 31) / 32;      // 32-row blocks of Oᵀ
+  constexpr int KP = D + 8;              // K row pitch (elements)
+  constexpr int VP = DB * 32 + 8;        // V row pitch; columns [D, 32 DB) stay zero
+  constexpr int NCH = D / 8;             // 16-B chunks per key row
+  constexpr int NST = (64 * NCH + 255) / 256;  // chunks per thread per tile (K and V each)
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[2][64 * KP];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[2][64 * VP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  int bx, by;
+  xcd_remap2(bx, by);
+  const int64_t bh = by;
+  const int64_t b = bh / heads, hd = bh % heads;
+  const int64_t bo = b / in.n, bi = b % in.n;
+  Q += bo * sq_b + bi * in.sq + hd * sq_h;
+  K += bo * sk_b + bi * in.sk + hd * sk_h;
+  V += bo * sv_b + bi * in.sv + hd * sv_h;
+  O += bo * so_b + bi * in.so + hd * so_h;
+
+  if constexpr (DB * 32 != D) {  // zero V's pad columns once (both buffers)
+    for (int i = tid; i < 2 * 64 * (DB * 32 - D); i += 256) {
+      const int buf = i / (64 * (DB * 32 - D)), rem = i % (64 * (DB * 32 - D));
+      Vs[buf][(rem / (DB * 32 - D)) * VP + D + rem % (DB * 32 - D)] = __bf16(0.f);
+    }
+  }
+
+  const int qrow = bx * 128 + wid * 32 + r;
+  bf16x8 qf[NKS];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s)
+    qf[s] = qrow < lq ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * sq_l + 16 * s + 8 * h) : bf16x8{};
+
+  f32x16 oacc[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) oacc[i] = f32x16{};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  uint4 kst[NST], vst[NST];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / NCH, c = idx % NCH;
+      const int key = t * 64 + row;
+      const bool ok = idx < 64 * NCH && key < lk;
+      kst[i] = ok ? *reinterpret_cast<const uint4*>(K + (int64_t)key * sk_l + 8 * c) : uint4{0, 0, 0, 0};
+      vst[i] = ok ? *reinterpret_cast<const uint4*>(V + (int64_t)key * sv_l + 8 * c) : uint4{0, 0, 0, 0};
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < 64 * NCH) {
+        const int row = idx / NCH, c = idx % NCH;
+        *reinterpret_cast<uint4*>(&Ks[buf][row * KP + 8 * c]) = kst[i];
+        *reinterpret_cast<uint4*>(&Vs[buf][row * VP + 8 * c]) = vst[i];
+      }
+    }
+  };
+  // per-lane part of the Vᵀ tr16 read address: 16-lane group g, lane 4q + p of it reads key row q,
+  // columns 4p..4p+3 of the group's 16-column slice
+  const int tg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const int voff = (4 * (tg >> 1) + tq) * VP + 16 * (tg & 1) + 4 * tp;
+
+  auto tile = [&](int t, int buf, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
+    const __bf16* ks = Ks[buf];
+    const __bf16* vs = Vs[buf];
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      sacc[kb] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(ks + (kb * 32 + r) * KP + 16 * s + 8 * h);
+        sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], sacc[kb], 0, 0, 0);
+      }
+    }
+    if constexpr (MASK) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (t * 64 + kb * 32 + (j & 3) + 8 * (j >> 2) + 4 * h >= lk) sacc[kb][j] = -INFINITY;
+    }
+    float mt = sacc[0][0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) mt = fmaxf(mt, sacc[0][j]);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mt = fmaxf(mt, sacc[1][j]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mt), __float_as_uint(mt), false, false);
+      mt = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    const float m_new = fmaxf(m_run, mt * scale_log2);
+    if (__ballot(m_new > m_run) != 0) {  // exact: alpha == 1 for every lane otherwise
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      l_run *= alpha;
+#pragma unroll
+      for (int i = 0; i < DB; ++i) oacc[i] *= alpha;
+      m_run = m_new;
+    }
+    float ls = 0.f;
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][j], scale_log2, -m_new));
+        sacc[kb][j] = p;
+        ls += p;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const f32x4 lo = {sacc[kb][8 * s], sacc[kb][8 * s + 1], sacc[kb][8 * s + 2], sacc[kb][8 * s + 3]};
+        const f32x4 hi = {sacc[kb][8 * s + 4], sacc[kb][8 * s + 5], sacc[kb][8 * s + 6], sacc[kb][8 * s + 7]};
+        pf[kb][s] = __builtin_shufflevector(__builtin_convertvector(lo, bf16x4), __builtin_convertvector(hi, bf16x4),
+                                            0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+    l_run += ls;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const __bf16* va = vs + (kb * 32 + 16 * s) * VP + voff;
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(va + 32 * db));
+          const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(va + 8 * VP + 32 * db));
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][s], oacc[db], 0, 0, 0);
+        }
+      }
+  };
+
+  const int ntiles = (lk + 63) / 64;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles - 1; ++t) {
+    gload(t + 1);  // lands during this tile's MFMAs
+    tile(t, t & 1, std::false_type{});
+    lstore((t + 1) & 1);  // that buffer's last reader (tile t - 1) finished before the last barrier
+    __syncthreads();
+  }
+  tile(ntiles - 1, (ntiles - 1) & 1, std::true_type{});
+
+  float l_tot = l_run;
+  {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_tot), __float_as_uint(l_tot), false, false);
+    l_tot = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  if (qrow < lq) {
+    const float inv = 1.f / l_tot;
+    __bf16* orow = O + (int64_t)qrow * so_l;
+#pragma unroll
+    for (int db = 0; db < DB; ++db)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int d0 = 32 * db + 8 * u + 4 * h;
+        if (d0 < D) {
+          const f32x4 w = {oacc[db][4 * u], oacc[db][4 * u + 1], oacc[db][4 * u + 2], oacc[db][4 * u + 3]};
+          *reinterpret_cast<bf16x4*>(orow + d0) = __builtin_convertvector(w * inv, bf16x4);
+        }
+      }
+    if (LSE && h == 0) LSE[bh * lq + qrow] = (m_run + log2f(l_tot)) * LN2;
+  }
+}
+
 // Short sequences (Lq, Lk <= 16: the tracker's per-track time attention over S = 16 frames,
 // blocks.py:312-321): one wave per (batch, head) instead of a 64 x 64 tile that would be 1/16
 // occupied. Sᵀ = K·Qᵀ in one 16x16 MFMA tile per 32 of d (K and Q fragments straight from
@@ -546,6 +742,17 @@ int launch_fwd_bf16(const comet_attn_args& a, hipStream_t s) {
   return COMET_OK;
 }
 
+template <int D>
+int launch_fwd32(const comet_attn_args& a, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(a.lq, 128), (unsigned)(a.batch * a.heads));
+  hipLaunchKernelGGL((attn_fwd32_kernel<D>), grid, dim3(256), 0, s,
+                     (const __bf16*)a.q, a.sq_b, a.sq_h, a.sq_l, (const __bf16*)a.k, a.sk_b, a.sk_h, a.sk_l,
+                     (const __bf16*)a.v, a.sv_b, a.sv_h, a.sv_l, (__bf16*)a.o, a.so_b, a.so_h, a.so_l,
+                     a.lse, (int)a.heads, (int)a.lq, (int)a.lk, a.scale * LOG2E, inner_of(a));
+  COMET_CHECK_LAUNCH("comet_attention_fwd (32x32)");
+  return COMET_OK;
+}
+
 template <typename T>
 int dispatch_d(const comet_attn_args& a, hipStream_t s) {
   if (std::is_same<T, __bf16>::value && a.lq <= 16 && a.lk <= 16 && a.batch * a.heads < (1ll << 31) * 4) {
@@ -554,6 +761,17 @@ int dispatch_d(const comet_attn_args& a, hipStream_t s) {
       case 48: return launch_small<48>(a, s);
       case 64: return launch_small<64>(a, s);
       case 96: return launch_small<96>(a, s);
+      default: break;
+    }
+  }
+  // 32x32x16 kernel for every bf16 shape past the one-wave kernel's; COMET_ATTN_FWD16=1 selects the
+  // 16x16x32 kernel (A/B measurement)
+  if (std::is_same<T, __bf16>::value && getenv("COMET_ATTN_FWD16") == nullptr) {
+    switch (a.head_dim) {
+      case 32: return launch_fwd32<32>(a, s);
+      case 48: return launch_fwd32<48>(a, s);
+      case 64: return launch_fwd32<64>(a, s);
+      case 96: return launch_fwd32<96>(a, s);
       default: break;
     }
   }
