@@ -40,6 +40,7 @@ struct Epi {
   void* aux; int64_t ldaux, sx0, sx1;
   float alpha; int act;
   int vec;  // output / resid / aux rows allow 8-wide vector access (host-checked)
+  int wide = 0;  // persistent kernel: 16-B bf16 stores (C 16-B aligned, ldc % 8 == 0; host-checked)
 };
 
 // Split-K partials: ws[((z * nb) + bz) * M * N + row * N + col], f32.
@@ -1017,6 +1018,11 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   // cost ~3-4 us per 256 x 256 tile, 10-18 % of a K = 384-768 GEMM). With GELU the parked path
   // serialises the activation behind the LDS round trips (+27 %): those keep the direct stores.
   constexpr bool PARK = std::is_same<TC, float>::value || (WCOLS % 64 == 0 && ACT == COMET_ACT_NONE);
+  // direct bf16 stores of interior tiles without a residual: fragments j, j+1 exchange halves by
+  // v_permlane16_swap so every lane stores 16 B (8 columns) instead of 8 B -- half the store
+  // instructions for the same bytes (the epilogue tail is store-issue bound: cdna_hip_programming.md
+  // T21). COMET_GEMM_NO_WIDE=1 at launch selects the 8-B stores (measurement A/B).
+  constexpr bool WIDE = !PARK && !HASR && std::is_same<TC, __bf16>::value && (NI % 2 == 0);
   // parked f32 row pitch: 64-wide slabs XOR-swizzle their 16-B chunks (c ^ pswz(r): the 8 rows
   // one ds_write_b128 lane group writes hit 8 distinct chunks and the 4 (row, 4-chunk) quads of
   // each ds_read_b128 lane group of the re-read are disjoint); 96-wide slabs pad rows to 100
@@ -1137,7 +1143,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (pend) {
       // VMEM ops per output kind of one epilogue: direct MI x NI, parked 2 x MI x (WCOLS / (8 * CPL))
-      constexpr int PER = PARK ? 2 * MI * (WCOLS / (8 * (16 / (int)sizeof(TC)))) : MI * NI;
+      constexpr int PER = PARK ? 2 * MI * (WCOLS / (8 * (16 / (int)sizeof(TC)))) : (WIDE ? MI * NI / 2 : MI * NI);
       constexpr int E = PER * (1 + (HASR ? 1 : 0)) + PER;  // C stores (+ resid loads) (+ aux stores)
       if constexpr (LN) {
         // C stores (+ resid loads) + one store per (row half, column pass) of each bf16 output
@@ -1494,12 +1500,52 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       if (interior) pepilogue(std::false_type{});
       else pepilogue(std::true_type{});
     } else {
+    if constexpr (WIDE) {
+      if (interior && X == nullptr && epi.wide) {
+        // lane (li, g) of fragment (i, j) holds row li, columns 16j + 4g .. +3 (bf16-packed as uint2);
+        // permlane16_swap(frag j, frag j+1) exchanges 16-lane groups 1 <-> 0 and 3 <-> 2, after which
+        // group g holds 8 contiguous columns: 16(j + (g & 1)) + 8(g >> 1) .. +7
+        const bool bias_c = epi.bias != nullptr;
+        float bc[NI][4];
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bc[j][e] = bias_c ? epi.bias[col0 + j * 16 + e] : 0.f;
+        const int64_t wcol = (int64_t)tn * TBN + wc * WCOLS + 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int64_t row = row0 + i * 16;
+#pragma unroll
+          for (int j = 0; j < NI; j += 2) {
+            unsigned pk[2][2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              float v[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = apply_act(ACT, epi.alpha * acc[i][j + u][e] + bc[j + u][e]);
+              pk[u][0] = pack_bf16x2(v[0], v[1]);
+              pk[u][1] = pack_bf16x2(v[2], v[3]);
+              acc[i][j + u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+            *reinterpret_cast<uint4*>(C + row * ldc + wcol + 16 * j) = uint4{s0[0], s1[0], s0[1], s1[1]};
+          }
+        }
+      } else if (interior) {
+        epilogue(std::false_type{});
+      } else {
+        epilogue(std::true_type{});
+      }
+    } else {
     if (interior) epilogue(std::false_type{});
     else epilogue(std::true_type{});
     }
+    }
     // interior: every VMEM op this epilogue issued came after the LDS-DMA of k-tile q+2 and their
     // count is fixed, so the next barrier wait leaves them in flight
-    pend = interior ? 1 : 0;
+    if constexpr (WIDE) pend = (interior && X == nullptr && epi.wide) ? 1 : 0;
+    else pend = interior ? 1 : 0;
   }
 }
 }  // namespace w4
@@ -1602,6 +1648,7 @@ int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s
 template <typename TC>
 int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
+  e.wide = (uintptr_t)a.c % 16 == 0 && a.ldc % 8 == 0 && getenv("COMET_GEMM_NO_WIDE") == nullptr;
   const w4::RowLN noln{};
   // N = 384 (the tracker's hidden size): 128 x 384 tiles (each A row block read once);
   // otherwise 256 x 256

@@ -512,6 +512,14 @@ def test_gemm_256_tile_path(mnk, epi):
     if epi == "plain_f32":
         out = ops.linear(x.to(DEV), w.to(DEV), out_dtype=torch.float32)
         _close(out, pre, 1e-4, 1e-4 * math.sqrt(K), f"256 plain {mnk}")
+    elif epi == "gelu_bf16":
+        # interior tiles store 16 B per lane (permlane16 pairs), edge tiles 8 B: both against f64,
+        # and the wide stores bit-identical to the 8-B ones (COMET_GEMM_NO_WIDE=1)
+        out = ops.linear(xd, wd, bias=bd, act=1, out_dtype=torch.bfloat16)
+        _close(out, F.gelu(pre + b.double()), 1e-2, 1e-2, f"pp gelu {mnk}")
+        monkeypatch.setenv("COMET_GEMM_NO_WIDE", "1")
+        out8 = ops.linear(xd, wd, bias=bd, act=1, out_dtype=torch.bfloat16)
+        assert torch.equal(out, out8), f"wide vs 8-B stores differ at {mnk}"
     elif epi == "gelu_aux_bf16":
         aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         out = ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=1, aux=aux, out_dtype=torch.bfloat16)
@@ -526,8 +534,8 @@ def test_gemm_256_tile_path(mnk, epi):
 @pytest.mark.parametrize("mnk", [(20000, 3072, 192), (70001, 768, 64), (33000, 1152, 256), (4100, 1024, 1536),
                                  (20001, 384, 1536), (8200, 384, 384), (65536, 384, 64),
                                  (8192, 1536, 384), (6000, 768, 192), (8200, 1152, 320)])
-@pytest.mark.parametrize("epi", ["plain_f32", "gelu_aux_bf16", "bias_resid_f32", "inplace_resid_f32"])
-def test_gemm_persistent_path(mnk, epi):
+@pytest.mark.parametrize("epi", ["plain_f32", "gelu_aux_bf16", "gelu_bf16", "bias_resid_f32", "inplace_resid_f32"])
+def test_gemm_persistent_path(mnk, epi, monkeypatch):
     """Persistent kernel (256 x 256 tiles; 128 x 384 for N = 384): several tiles per workgroup
     (k-tile prefetch across tile boundaries), M / N tails, direct (bf16) and parked (f32) epilogues
     incl. an in-place residual (out is resid), vs f64."""

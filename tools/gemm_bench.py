@@ -66,11 +66,17 @@ def main():
         del os.environ["COMET_GEMM_NO_SK"]
         t = bench(lambda: ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt))
         err = (out.float() - ref_out.float()).abs().max().item()
+        extra = ""
+        if os.environ.get("COMET_GEMM_AB"):  # A/B switch named by COMET_GEMM_AB (e.g. COMET_GEMM_NO_WIDE)
+            os.environ[os.environ["COMET_GEMM_AB"]] = "1"
+            tb = bench(lambda: ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt))
+            del os.environ[os.environ["COMET_GEMM_AB"]]
+            extra = f" | {os.environ['COMET_GEMM_AB']} {fl_ / tb / 1e9 if (fl_ := 2.0 * M * N * K) else 0:6.0f} TF/s"
         tt = bench(lambda: torch.matmul(x, w.t()))
         fl = 2.0 * M * N * K
         print(f"{M:6d} {N:5d} {K:5d} {act:3d} {str(odt)[6:]:>4} {int(res):3d} | {t:8.3f} {fl / t / 1e9:6.0f} | "
               f"{tt:8.3f} {fl / tt / 1e9:5.0f} | {tt / t:5.2f} | no-SK {fl / t_pp / 1e9:6.0f} | 256-row {fl / t_old / 1e9:6.0f} TF/s, "
-              f"max|new-old| {err:.2e}", flush=True)
+              f"max|new-old| {err:.2e}{extra}", flush=True)
 
 
 if __name__ == "__main__":
