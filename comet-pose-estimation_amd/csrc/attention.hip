@@ -610,21 +610,27 @@ attn_fwd32_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_tot), __float_as_uint(l_tot), false, false);
     l_tot = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
   }
-  if (qrow < lq) {
-    const float inv = 1.f / l_tot;
-    __bf16* orow = O + (int64_t)qrow * so_l;
+  // O rows: lane (r, h) holds d = 32 db + 8u + 4h + (0..3); a v_permlane32_swap per dword of the
+  // (u, u + 1) pair gives each lane 8 contiguous d (16-B stores, cdna_hip_programming.md T21)
+  const float inv = 1.f / l_tot;
+  __bf16* orow = O + (int64_t)qrow * so_l;
 #pragma unroll
-    for (int db = 0; db < DB; ++db)
+  for (int db = 0; db < DB; ++db)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int d0 = 32 * db + 8 * u + 4 * h;
-        if (d0 < D) {
-          const f32x4 w = {oacc[db][4 * u], oacc[db][4 * u + 1], oacc[db][4 * u + 2], oacc[db][4 * u + 3]};
-          *reinterpret_cast<bf16x4*>(orow + d0) = __builtin_convertvector(w * inv, bf16x4);
-        }
+    for (int u = 0; u < 4; u += 2) {
+      if (32 * db + 8 * u >= D) continue;  // D % 16 == 0: a pair is all in or all out
+      uint2 pk[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x4 w = f32x4{oacc[db][4 * (u + e)], oacc[db][4 * (u + e) + 1], oacc[db][4 * (u + e) + 2],
+                              oacc[db][4 * (u + e) + 3]} * inv;
+        pk[e] = __builtin_bit_cast(uint2, __builtin_convertvector(w, bf16x4));
       }
-    if (LSE && h == 0) LSE[bh * lq + qrow] = (m_run + log2f(l_tot)) * LN2;
-  }
+      const auto sx = __builtin_amdgcn_permlane32_swap(pk[0].x, pk[1].x, false, false);
+      const auto sy = __builtin_amdgcn_permlane32_swap(pk[0].y, pk[1].y, false, false);
+      if (qrow < lq) *reinterpret_cast<uint4*>(orow + 32 * db + 8 * u + 8 * h) = uint4{sx[0], sy[0], sx[1], sy[1]};
+    }
+  if (LSE && h == 0 && qrow < lq) LSE[bh * lq + qrow] = (m_run + log2f(l_tot)) * LN2;
 }
 
 // Short sequences (Lq, Lk <= 16: the tracker's per-track time attention over S = 16 frames,

@@ -18,6 +18,8 @@
 //    ds_read_b64_tr_b16.
 // The k index of the P/dS operands is permuted (32u + 4g + j, 32u + 16 + 4g + j) identically
 // on both MFMA operands, as in the forward's P·V.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace comet {
@@ -347,6 +349,310 @@ attn_bwd_dq2_kernel(BwdPtrs p) {
   }
 }
 
+// ---------------------------------------------------------------- 32x32x16 MFMA kernels
+// Same two-kernel split, on v_mfma_f32_32x32x16_bf16 (half the vector-issue cost per FLOP of the
+// 16x16x32 form, twice the operand reuse per LDS fragment), one barrier per tile (the next tile's
+// global loads are issued before this tile's MFMAs and written to the other LDS buffer after them):
+//  * dkdv32: one wave = 32 keys (K / V fragments in registers), workgroup = 128 keys; per 32-query
+//    block S = Q·Kᵀ and dP = dO·Vᵀ with the key on the lane (queries in the registers), then
+//    dVᵀ += dOᵀ·P and dKᵀ += Qᵀ·dS with P / dS straight from the accumulators as B operands and
+//    the dOᵀ / Qᵀ A fragments read transposed (ds_read_b64_tr_b16) in the accumulator's permuted
+//    query order;
+//  * dq32: one wave = 32 queries (Q / dO fragments in registers, lse / Δ lane-local), per 32-key
+//    block Sᵀ = K·Qᵀ, dPᵀ = V·dOᵀ, dQᵀ += Kᵀ·dSᵀ.
+// Outputs leave as 16-B rows: lane pairs (l, l + 32) swap halves with v_permlane32_swap.
+typedef __attribute__((ext_vector_type(16))) float f32x16b;
+
+template <int D> struct B32 {
+  static constexpr int NKS = D / 16;              // k-steps over d of S / dP
+  static constexpr int DB = (D + 31) / 32;        // 32-row output blocks over d
+  static constexpr int TP = D + 8;                // LDS row pitch of the Q / dO (K / V) tiles
+  static constexpr int TPV = DB * 32 + 8;         // pitch of tiles read transposed (pad cols zero)
+  static constexpr int NCH = D / 8;               // 16-B chunks per row
+  static constexpr int NST = (64 * NCH + 255) / 256;
+};
+
+// 16 consecutive-d values of a [d-block][lane] accumulator row set -> one 16-B row store per lane
+// pair: lane (r, h) holds d = 32 db + 8u + 4h + (0..3) of its row r
+template <int D>
+__device__ __forceinline__ void store_rows32(__bf16* row_ptr, bool ok, const f32x16b (&acc)[B32<D>::DB], float mul, int h) {
+#pragma unroll
+  for (int db = 0; db < B32<D>::DB; ++db)
+#pragma unroll
+    for (int u = 0; u < 4; u += 2) {
+      if (32 * db + 8 * u >= D) continue;
+      uint2 pk[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const f32x4 w = f32x4{acc[db][4 * (u + e)], acc[db][4 * (u + e) + 1], acc[db][4 * (u + e) + 2],
+                              acc[db][4 * (u + e) + 3]} * mul;
+        pk[e] = __builtin_bit_cast(uint2, __builtin_convertvector(w, bf16x4));
+      }
+      const auto sx = __builtin_amdgcn_permlane32_swap(pk[0].x, pk[1].x, false, false);
+      const auto sy = __builtin_amdgcn_permlane32_swap(pk[0].y, pk[1].y, false, false);
+      if (ok) *reinterpret_cast<uint4*>(row_ptr + 32 * db + 8 * u + 8 * h) = uint4{sx[0], sy[0], sx[1], sy[1]};
+    }
+}
+
+__device__ __forceinline__ bf16x8 pack16(const f32x16b& x, int s) {
+  const f32x4 lo = {x[8 * s], x[8 * s + 1], x[8 * s + 2], x[8 * s + 3]};
+  const f32x4 hi = {x[8 * s + 4], x[8 * s + 5], x[8 * s + 6], x[8 * s + 7]};
+  return __builtin_shufflevector(__builtin_convertvector(lo, bf16x4), __builtin_convertvector(hi, bf16x4), 0, 1, 2, 3,
+                                 4, 5, 6, 7);
+}
+
+// A fragment of k-step s (16 rows: r0 + 16s + 8(j>>2) + 4h + (j&3)) x 32 columns (c0 + lane's 16-lane
+// group slice) of a row-major LDS tile, transposed (Xᵀ rows = columns of the tile)
+__device__ __forceinline__ bf16x8 frag_tr32(const __bf16* tile, int pitch, int r0, int c0, int lane) {
+  const int tg = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+  const __bf16* a = tile + (r0 + 4 * (tg >> 1) + tq) * pitch + c0 + 16 * (tg & 1) + 4 * tp;
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4b*)(a));
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4b*)(a + 8 * pitch));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+attn_bwd_dkdv32_kernel(BwdPtrs p) {
+  typedef B32<D> C;
+  constexpr int NKS = C::NKS, DB = C::DB, TP = C::TPV, NCH = C::NCH, NST = C::NST;
+  __shared__ __attribute__((aligned(16))) __bf16 Qs[2][64 * TP];
+  __shared__ __attribute__((aligned(16))) __bf16 Gs[2][64 * TP];
+  __shared__ __attribute__((aligned(16))) float lse_s[2][64];
+  __shared__ __attribute__((aligned(16))) float dl_s[2][64];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  int bx, by;
+  xcd_remap2(bx, by);
+  const int64_t bh = by, b = bh / p.heads, hd = bh % p.heads;
+  const __bf16* Q = p.q + b * p.sq_b + hd * p.sq_h;
+  const __bf16* K = p.k + b * p.sk_b + hd * p.sk_h;
+  const __bf16* V = p.v + b * p.sv_b + hd * p.sv_h;
+  const __bf16* Gd = p.dout + b * p.sd_b + hd * p.sd_h;
+  const float* LSE = p.lse + bh * p.lq;
+  const float* DL = p.delta + bh * p.lq;
+  const float sl2 = p.scale * LOG2E_B;
+
+  if constexpr (DB * 32 != D) {  // pad columns of the tiles read transposed stay zero
+    constexpr int PADC = DB * 32 - D;
+    for (int i = tid; i < 2 * 64 * PADC; i += 256) {
+      const int buf = i / (64 * PADC), rem = i % (64 * PADC);
+      Qs[buf][(rem / PADC) * TP + D + rem % PADC] = __bf16(0.f);
+      Gs[buf][(rem / PADC) * TP + D + rem % PADC] = __bf16(0.f);
+    }
+  }
+
+  const int key = bx * 128 + wid * 32 + r;
+  const bool kok = key < p.lk;
+  bf16x8 kf[NKS], vf[NKS];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    kf[s] = kok ? *reinterpret_cast<const bf16x8*>(K + (int64_t)key * p.sk_l + 16 * s + 8 * h) : bf16x8{};
+    vf[s] = kok ? *reinterpret_cast<const bf16x8*>(V + (int64_t)key * p.sv_l + 16 * s + 8 * h) : bf16x8{};
+  }
+  f32x16b dv[DB], dk[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) { dv[i] = f32x16b{}; dk[i] = f32x16b{}; }
+
+  uint4 qst[NST], gst[NST];
+  float lreg = 0.f, dreg = 0.f;
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / NCH, c = idx % NCH;
+      const int q = t * 64 + row;
+      const bool ok = idx < 64 * NCH && q < p.lq;
+      qst[i] = ok ? *reinterpret_cast<const uint4*>(Q + (int64_t)q * p.sq_l + 8 * c) : uint4{0, 0, 0, 0};
+      gst[i] = ok ? *reinterpret_cast<const uint4*>(Gd + (int64_t)q * p.sd_l + 8 * c) : uint4{0, 0, 0, 0};
+    }
+    if (tid < 64) {
+      const int q = t * 64 + tid;
+      lreg = q < p.lq ? LSE[q] * LOG2E_B : INFINITY;  // queries past lq: P = 0
+      dreg = q < p.lq ? DL[q] : 0.f;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < 64 * NCH) {
+        const int row = idx / NCH, c = idx % NCH;
+        *reinterpret_cast<uint4*>(&Qs[buf][row * TP + 8 * c]) = qst[i];
+        *reinterpret_cast<uint4*>(&Gs[buf][row * TP + 8 * c]) = gst[i];
+      }
+    }
+    if (tid < 64) { lse_s[buf][tid] = lreg; dl_s[buf][tid] = dreg; }
+  };
+
+  auto tile = [&](int buf) {
+    const __bf16* qs = Qs[buf];
+    const __bf16* gs = Gs[buf];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      f32x16b sacc = f32x16b{}, pacc = f32x16b{};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(qs + (qb * 32 + r) * TP + 16 * s + 8 * h);
+        const bf16x8 ga = *reinterpret_cast<const bf16x8*>(gs + (qb * 32 + r) * TP + 16 * s + 8 * h);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[s], pacc, 0, 0, 0);
+      }
+      // register j: query qb*32 + 8(j>>2) + 4h + (j&3)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(&lse_s[buf][qb * 32 + 8 * u + 4 * h]);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&dl_s[buf][qb * 32 + 8 * u + 4 * h]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pr = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[4 * u + e], sl2, -l4[e]));
+          sacc[4 * u + e] = pr;                               // P
+          pacc[4 * u + e] = pr * (pacc[4 * u + e] - d4[e]);   // dS (unscaled)
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 pb = pack16(sacc, s2), sb = pack16(pacc, s2);
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const bf16x8 ga = frag_tr32(gs, TP, qb * 32 + 16 * s2, 32 * db, lane);
+          const bf16x8 qa = frag_tr32(qs, TP, qb * 32 + 16 * s2, 32 * db, lane);
+          dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, pb, dv[db], 0, 0, 0);
+          dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, sb, dk[db], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  const int ntiles = (p.lq + 63) / 64;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    tile(t & 1);
+    if (t + 1 < ntiles) lstore((t + 1) & 1);
+    __syncthreads();
+  }
+  __bf16* dK = p.dk + b * p.sdk_b + hd * p.sdk_h + (int64_t)key * p.sdk_l;
+  __bf16* dV = p.dv + b * p.sdv_b + hd * p.sdv_h + (int64_t)key * p.sdv_l;
+  store_rows32<D>(dV, kok, dv, 1.f, h);
+  store_rows32<D>(dK, kok, dk, p.scale, h);
+}
+
+template <int D>
+__global__ void __launch_bounds__(256, 2)
+attn_bwd_dq32_kernel(BwdPtrs p) {
+  typedef B32<D> C;
+  constexpr int NKS = C::NKS, DB = C::DB, TP = C::TPV, NCH = C::NCH, NST = C::NST;
+  __shared__ __attribute__((aligned(16))) __bf16 Ks[2][64 * TP];
+  __shared__ __attribute__((aligned(16))) __bf16 Vs[2][64 * TP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  int bx, by;
+  xcd_remap2(bx, by);
+  const int64_t bh = by, b = bh / p.heads, hd = bh % p.heads;
+  const __bf16* Q = p.q + b * p.sq_b + hd * p.sq_h;
+  const __bf16* K = p.k + b * p.sk_b + hd * p.sk_h;
+  const __bf16* V = p.v + b * p.sv_b + hd * p.sv_h;
+  const __bf16* Gd = p.dout + b * p.sd_b + hd * p.sd_h;
+  const float sl2 = p.scale * LOG2E_B;
+
+  if constexpr (DB * 32 != D) {
+    constexpr int PADC = DB * 32 - D;
+    for (int i = tid; i < 2 * 64 * PADC; i += 256) {
+      const int buf = i / (64 * PADC), rem = i % (64 * PADC);
+      Ks[buf][(rem / PADC) * TP + D + rem % PADC] = __bf16(0.f);
+    }
+  }
+
+  const int qrow = bx * 128 + wid * 32 + r;
+  const bool qok = qrow < p.lq;
+  bf16x8 qf[NKS], gf[NKS];
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    qf[s] = qok ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * p.sq_l + 16 * s + 8 * h) : bf16x8{};
+    gf[s] = qok ? *reinterpret_cast<const bf16x8*>(Gd + (int64_t)qrow * p.sd_l + 16 * s + 8 * h) : bf16x8{};
+  }
+  const float lse2 = qok ? p.lse[bh * p.lq + qrow] * LOG2E_B : INFINITY;
+  const float dl = qok ? p.delta[bh * p.lq + qrow] : 0.f;
+  f32x16b acc[DB];
+#pragma unroll
+  for (int i = 0; i < DB; ++i) acc[i] = f32x16b{};
+
+  uint4 kst[NST], vst[NST];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int idx = tid + i * 256;
+      const int row = idx / NCH, c = idx % NCH;
+      const int kk = t * 64 + row;
+      const bool ok = idx < 64 * NCH && kk < p.lk;
+      kst[i] = ok ? *reinterpret_cast<const uint4*>(K + (int64_t)kk * p.sk_l + 8 * c) : uint4{0, 0, 0, 0};
+      vst[i] = ok ? *reinterpret_cast<const uint4*>(V + (int64_t)kk * p.sv_l + 8 * c) : uint4{0, 0, 0, 0};
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int idx = tid + i * 256;
+      if (idx < 64 * NCH) {
+        const int row = idx / NCH, c = idx % NCH;
+        *reinterpret_cast<uint4*>(&Ks[buf][row * TP + 8 * c]) = kst[i];
+        *reinterpret_cast<uint4*>(&Vs[buf][row * TP + 8 * c]) = vst[i];
+      }
+    }
+  };
+
+  auto tile = [&](int t, int buf) {
+    const __bf16* ks = Ks[buf];
+    const __bf16* vs = Vs[buf];
+    const bool ragged = t * 64 + 64 > p.lk;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      f32x16b sacc = f32x16b{}, pacc = f32x16b{};
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(ks + (kb * 32 + r) * TP + 16 * s + 8 * h);
+        const bf16x8 va = *reinterpret_cast<const bf16x8*>(vs + (kb * 32 + r) * TP + 16 * s + 8 * h);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[s], sacc, 0, 0, 0);
+        pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, gf[s], pacc, 0, 0, 0);
+      }
+      // register j: key t*64 + kb*32 + 8(j>>2) + 4h + (j&3)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        float pr = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j], sl2, -lse2));
+        if (ragged && t * 64 + kb * 32 + 8 * (j >> 2) + 4 * h + (j & 3) >= p.lk) pr = 0.f;
+        pacc[j] = pr * (pacc[j] - dl);  // dS (unscaled)
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 sb = pack16(pacc, s2);
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const bf16x8 ka = frag_tr32(ks, TP, kb * 32 + 16 * s2, 32 * db, lane);
+          acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, sb, acc[db], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  const int ntiles = (p.lk + 63) / 64;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 1 < ntiles) gload(t + 1);
+    tile(t, t & 1);
+    if (t + 1 < ntiles) lstore((t + 1) & 1);
+    __syncthreads();
+  }
+  __bf16* dQ = p.dq + b * p.sdq_b + hd * p.sdq_h + (int64_t)qrow * p.sdq_l;
+  store_rows32<D>(dQ, qok, acc, p.scale, h);
+}
+
 // Δ = rowsum(dO ∘ O), one wave per 4 query rows... one lane group of 8 per row (D <= 128)
 __global__ void __launch_bounds__(256)
 attn_delta_bf16_kernel(const __bf16* __restrict__ dO, const __bf16* __restrict__ O, float* __restrict__ delta,
@@ -371,6 +677,15 @@ attn_delta_bf16_kernel(const __bf16* __restrict__ dO, const __bf16* __restrict__
   acc += __shfl_xor(acc, 2, 64);
   acc += __shfl_xor(acc, 4, 64);
   if (r < rows && sub == 0) delta[r] = acc;
+}
+
+template <int D>
+int launch_bwd32(const BwdPtrs& p, int64_t bh, hipStream_t s) {
+  hipLaunchKernelGGL((attn_bwd_dkdv32_kernel<D>), dim3((unsigned)cdiv(p.lk, 128), (unsigned)bh), dim3(256), 0, s, p);
+  COMET_CHECK_LAUNCH("comet_attention_bwd (dk, dv; 32x32)");
+  hipLaunchKernelGGL((attn_bwd_dq32_kernel<D>), dim3((unsigned)cdiv(p.lq, 128), (unsigned)bh), dim3(256), 0, s, p);
+  COMET_CHECK_LAUNCH("comet_attention_bwd (dq; 32x32)");
+  return COMET_OK;
 }
 
 template <int D>
@@ -414,6 +729,18 @@ extern "C" int comet_attention_bwd(const comet_attn_bwd_args* args, void* stream
             (const __bf16*)a.v, a.sv_b, a.sv_h, a.sv_l, (const __bf16*)a.dout, a.sd_b, a.sd_h, a.sd_l,
             (__bf16*)a.dq, a.sdq_b, a.sdq_h, a.sdq_l, (__bf16*)a.dk, a.sdk_b, a.sdk_h, a.sdk_l,
             (__bf16*)a.dv, a.sdv_b, a.sdv_h, a.sdv_l, a.lse, a.delta, (int)a.heads, (int)a.lq, (int)a.lk, a.scale};
+  // 32x32x16 kernels (16-B dK / dV / dQ row stores: 16-B aligned outputs); COMET_ATTN_BWD16=1
+  // selects the 16x16x32 kernels (A/B measurement)
+  const bool wide = ((uintptr_t)a.dk | (uintptr_t)a.dv) % 16 == 0 && getenv("COMET_ATTN_BWD16") == nullptr;
+  if (wide) {
+    switch (a.head_dim) {
+      case 32: return launch_bwd32<32>(p, bh, s);
+      case 48: return launch_bwd32<48>(p, bh, s);
+      case 64: return launch_bwd32<64>(p, bh, s);
+      case 96: return launch_bwd32<96>(p, bh, s);
+      default: break;
+    }
+  }
   switch (a.head_dim) {
     case 32: return launch_bwd<32>(p, bh, s);
     case 48: return launch_bwd<48>(p, bh, s);

@@ -21,6 +21,8 @@ SHAPES = [
     ("tracker p2v", 128, 8, 512, 64, 48, False),
     ("tracker v2p", 128, 8, 64, 512, 48, False),
     ("tracker virt", 128, 8, 64, 64, 48, False),
+    ("trunk", 8, 8, 16, 16, 96, True),
+    ("T_P cross", 128, 8, 1, 512, 96, True),
     ("long T64 768", 4, 12, 64 * 37 * 37 // 64 + 1, 64 * 37 * 37 // 64 + 1, 64, False),
 ]
 
@@ -60,6 +62,11 @@ def main():
             dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
             msb = timeit(lambda: ops.attention_bwd(q, k, v, o, lse, do, H, D ** -0.5, dq, dk, dv))
             line += f"  bwd {msb * 1e3:8.1f} us {2.5 * fl / msb / 1e9:7.1f} TF/s"
+            if os.environ.get("COMET_ATTN_AB"):  # the 16x16x32 backward kernels
+                os.environ["COMET_ATTN_BWD16"] = "1"
+                msb16 = timeit(lambda: ops.attention_bwd(q, k, v, o, lse, do, H, D ** -0.5, dq, dk, dv))
+                del os.environ["COMET_ATTN_BWD16"]
+                line += f" (16x16: {msb16 * 1e3:8.1f} us {2.5 * fl / msb16 / 1e9:7.1f})"
         print(line, flush=True)
 
 
