@@ -731,7 +731,10 @@ extern "C" int comet_attention_bwd(const comet_attn_bwd_args* args, void* stream
             (__bf16*)a.dv, a.sdv_b, a.sdv_h, a.sdv_l, a.lse, a.delta, (int)a.heads, (int)a.lq, (int)a.lk, a.scale};
   // 32x32x16 kernels (16-B dK / dV / dQ row stores: 16-B aligned outputs); COMET_ATTN_BWD16=1
   // selects the 16x16x32 kernels (A/B measurement)
-  const bool wide = ((uintptr_t)a.dk | (uintptr_t)a.dv) % 16 == 0 && getenv("COMET_ATTN_BWD16") == nullptr;
+  // (128-row workgroups: short query / key sequences -- T_P's Lq = 1, the trunk's 16 -- stay on
+  // the 64-row kernels)
+  const bool wide = ((uintptr_t)a.dk | (uintptr_t)a.dv) % 16 == 0 && a.lq >= 64 && a.lk >= 64 &&
+                    getenv("COMET_ATTN_BWD16") == nullptr;
   if (wide) {
     switch (a.head_dim) {
       case 32: return launch_bwd32<32>(p, bh, s);
