@@ -102,7 +102,11 @@ def test_gemm_splitk_epilogue_batched(dtype):
                                  (200, 16, 16, 32, 32, 3, 1, 1), (100, 31, 31, 8, 32, 3, 2, 1), (64, 20, 20, 16, 64, 3, 1, 1),
                                  (300, 16, 16, 32, 32, 1, 2, 0), (70, 30, 30, 8, 48, 3, 1, 1),
                                  # 128 x 64 (N <= 64) tile: the BasicEncoder's 64 -> 64 convolutions
-                                 (4, 40, 40, 64, 64, 3, 1, 1), (3, 21, 19, 64, 56, 3, 1, 1)])
+                                 (4, 40, 40, 64, 64, 3, 1, 1), (3, 21, 19, 64, 56, 3, 1, 1),
+                                 # rows-in-LDS 3x3 kernel (c = cout = 64, w % 32 == 0, n*h >= 256): row
+                                 # ranges of 2 rows cross image boundaries; w = 128 (the encoder's)
+                                 (3, 100, 96, 64, 64, 3, 1, 1), (2, 130, 128, 64, 64, 3, 1, 1),
+                                 (1, 300, 32, 64, 64, 3, 1, 1)])
 @pytest.mark.parametrize("epi", ["bias", "bias_relu_resid"])
 def test_conv2d_nhwc_implicit_gemm(geo, epi):
     """comet_conv2d_nhwc (implicit GEMM, bf16) vs torch conv2d in f64 on the same bf16 inputs."""
@@ -124,6 +128,32 @@ def test_conv2d_nhwc_implicit_gemm(geo, epi):
         kw.update(act=2, resid=r.to(DEV), beta=0.5)
     y = ops.conv2d_nhwc(xd, wm.to(DEV), k, k, s, p, **kw)
     _close(y, ref, 1e-3, 1e-3, f"conv {geo} {epi}")
+
+
+@pytest.mark.parametrize("resid", [False, True])
+def test_conv3_rows_bf16_out_matches_generic_path(resid, monkeypatch):
+    """bf16 output of the rows-in-LDS 3x3 kernel (BasicEncoder 64 -> 64 at 128 x 128) vs f64 and
+    vs the implicit-GEMM path (COMET_CONV_NO_ROWS=1) on the same inputs: both round the same f32
+    sums to bf16, so they differ by at most one bf16 ulp where the summation order flips it."""
+    ops = _ops()
+    n, h, w, c = 2, 128, 128, 64
+    x = _rand(n, c, h, w, seed=24).to(torch.bfloat16)
+    wt = _rand(c, c, 3, 3, seed=25, scale=1.0 / math.sqrt(c * 9)).to(torch.bfloat16)
+    b = _rand(c, seed=26)
+    ref = F.conv2d(x.double(), wt.double(), b.double(), padding=1).permute(0, 2, 3, 1)
+    wm = wt.permute(0, 2, 3, 1).reshape(c, 9 * c).contiguous().to(DEV)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    kw = dict(bias=b.to(DEV), out_dtype=torch.bfloat16)
+    if resid:
+        r = _rand(*ref.shape, seed=27).to(torch.bfloat16)
+        ref = F.relu(ref) + 0.5 * r.double()
+        kw.update(act=2, resid=r.to(DEV), beta=0.5)
+    y = ops.conv2d_nhwc(xd, wm, 3, 3, 1, 1, **kw)
+    _close(y, ref, 1e-2, 1e-2, f"conv rows bf16 resid={resid}")
+    monkeypatch.setenv("COMET_CONV_NO_ROWS", "1")
+    y2 = ops.conv2d_nhwc(xd, wm, 3, 3, 1, 1, **kw)
+    d = (y.float() - y2.float()).abs()
+    assert (d <= 2 ** -7 * y2.float().abs() + 1e-6).all(), f"rows vs generic: max diff {d.max().item():.3e}"
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

@@ -51,11 +51,12 @@ def main():
         ms = timeit(lambda: ops.attention(q, k, v, H, D ** -0.5, lse=True))
         fl = 4.0 * B * H * Lq * Lk * D
         line = f"{name:14s} B{B:4d} H{H:3d} Lq{Lq:5d} Lk{Lk:5d} D{D:3d}  fwd {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s"
-        if os.environ.get("COMET_ATTN_AB"):  # the 16x16x32 forward kernel on the same shape
-            os.environ["COMET_ATTN_FWD16"] = "1"
-            ms16 = timeit(lambda: ops.attention(q, k, v, H, D ** -0.5, lse=True))
-            del os.environ["COMET_ATTN_FWD16"]
-            line += f" (16x16: {ms16 * 1e3:8.1f} us {fl / ms16 / 1e9:7.1f})"
+        if os.environ.get("COMET_ATTN_AB"):  # both forward kernels forced on the same shape
+            for var, tag in (("COMET_ATTN_FWD16", "16x16"), ("COMET_ATTN_FWD32", "32x32")):
+                os.environ[var] = "1"
+                msx = timeit(lambda: ops.attention(q, k, v, H, D ** -0.5, lse=True))
+                del os.environ[var]
+                line += f" ({tag}: {msx * 1e3:7.1f} us {fl / msx / 1e9:6.1f})"
         if bwd:
             o, lse = ops.attention(q, k, v, H, D ** -0.5, lse=True)
             do = torch.randn_like(o)
