@@ -44,8 +44,8 @@ def parse():
     ap.add_argument("--fwd-only", action="store_true",
                     help="BASELINE configs[1]: full COMET forward only (eval, no_grad), no loss backward / optimizer")
     ap.add_argument("--cpu-baseline-only", action="store_true")
-    ap.add_argument("--cpu-baseline-full", action="store_true",
-                    help="every SURVEY 8(d) CPU mode (train/eval x fp32/bf16), 2 reps each (default line: train fp32 only)")
+    ap.add_argument("--cpu-baseline-quick", action="store_true",
+                    help="CPU baseline of train bf16 only, 1 rep (default: every SURVEY 8(d) mode, 2 reps each)")
     ap.add_argument("--launcher-check", action="store_true",
                     help="CPU self-test of the --gpus N launcher: gloo ranks, one bucketed gradient all-reduce, no GPU")
     return ap.parse_args()
@@ -139,8 +139,8 @@ def synthetic(B, T, S_img, N, device, seed):
 
 
 CPU_MODES = {
-    "train_fp32": "train step fwd+bwd+clip+AdamW, fp32",
     "train_bf16": "train step fwd+bwd+clip+AdamW, bf16 autocast",
+    "train_fp32": "train step fwd+bwd+clip+AdamW, fp32",
     "eval_fp32": "eval forward (no_grad), fp32",
     "eval_bf16": "eval forward (no_grad), bf16 autocast",
 }
@@ -187,6 +187,9 @@ def oracle_timer(T, S_img, N):
     def run(mode):
         kind, prec = mode.split("_")
         ctx = torch.autocast("cpu", dtype=torch.bfloat16) if prec == "bf16" else torch.autocast("cpu", enabled=False)
+        # the reference turns autograd anomaly detection on in every camera-head forward
+        # (camera_predictor10.py:305) and leaves it on: the timed restatement runs in the same mode
+        torch.autograd.set_detect_anomaly(True)
         t0 = time.perf_counter()
         with ctx:
             if kind == "train":
@@ -194,15 +197,18 @@ def oracle_timer(T, S_img, N):
             else:
                 with torch.no_grad():
                     O.comet_forward(P, img, tracks, gt)
-        return time.perf_counter() - t0
+        el = time.perf_counter() - t0
+        torch.autograd.set_detect_anomaly(False)
+        return el
     return run
 
 
-def cpu_baseline(T, S_img, N, modes=("train_fp32",), reps=1, warmup_frames=4):
+def cpu_baseline(T, S_img, N, modes=tuple(CPU_MODES), reps=2, warmup_frames=4):
     """The oracle timed on this host's cores: per mode one warm-up (a T=`warmup_frames`
     sequence: thread pool, allocator and first-call costs, bounded) then `reps` timed sequences at
-    the full size; value = 1 / mean seconds. The default bench line is the bounded headline sample
-    (train fp32, 1 rep, ~20 s); `--cpu-baseline-full` runs every mode with 2 reps."""
+    the full size; value = 1 / mean seconds of the first mode (train bf16: the precision of the GPU
+    line). Default: every 8(d) mode (train / eval x fp32 / bf16), 2 reps each (~2 min of CPU);
+    `--cpu-baseline-quick` times train bf16 once."""
     threads = cpu_threads()
     torch.set_num_threads(threads)
     print(f"[bench] cpu baseline: oracle {list(modes)} on {threads} threads ...", file=sys.stderr, flush=True)
@@ -216,9 +222,10 @@ def cpu_baseline(T, S_img, N, modes=("train_fp32",), reps=1, warmup_frames=4):
     main_mode = modes[0]
     cpu = cpu_host()
     out = {"value": res[main_mode]["value"], "unit": "sequences/s", "cores": torch.get_num_threads(), "kind": "port",
-           "sample": f"B=1 sequence (T={T}, {S_img}x{S_img}, N={N}) {CPU_MODES[main_mode]}, oracle/comet_oracle.py, "
-                     f"1 warm-up (T={warmup_frames}) + {reps} timed, {sum(res[main_mode]['s_per_seq']) / reps:.1f} s/seq, "
-                     f"host '{cpu}'"}
+           "sample": f"B=1 sequence (T={T}, {S_img}x{S_img}, N={N}) {CPU_MODES[main_mode]}, oracle/comet_oracle.py "
+                     f"(autograd anomaly mode on, as the reference), 1 warm-up (T={warmup_frames}) + {reps} timed, "
+                     f"{sum(res[main_mode]['s_per_seq']) / reps:.1f} s/seq, host '{cpu}'; calibration against the "
+                     f"reference on the build container: profiles/r03_cpu_calibration.json"}
     if len(modes) > 1:
         out["modes"] = res
     return out
@@ -243,8 +250,8 @@ def pmc_traffic(instance, config):
 
 def main():
     args = parse()
-    cpu_modes = tuple(CPU_MODES) if args.cpu_baseline_full else ("train_fp32",)
-    cpu_reps = 2 if args.cpu_baseline_full else 1
+    cpu_modes = ("train_bf16",) if args.cpu_baseline_quick else tuple(CPU_MODES)
+    cpu_reps = 1 if args.cpu_baseline_quick else 2
     if args.cpu_baseline_only:
         print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks, modes=cpu_modes, reps=cpu_reps)))
         return 0

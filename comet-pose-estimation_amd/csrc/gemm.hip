@@ -41,6 +41,7 @@ struct Epi {
   float alpha; int act;
   int vec;  // output / resid / aux rows allow 8-wide vector access (host-checked)
   int wide = 0;  // persistent kernel: 16-B bf16 stores (C 16-B aligned, ldc % 8 == 0; host-checked)
+  int prio = 0;  // persistent kernel: s_setprio 1 for waves 4-7 (COMET_GEMM_PRIO=1, measurement)
 };
 
 // Split-K partials: ws[((z * nb) + bz) * M * N + row * N + col], f32.
@@ -1112,6 +1113,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
   };
 
+  // static priority for the younger half of the workgroup (cdna_hip_programming.md T5, static
+  // form): the second-dispatched waves lose VALU / issue arbitration on every segment otherwise
+  if (epi.prio && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   int pend = 0;  // 1: the last epilogue's stores are the newest VMEM ops (count known)
   // ---- prologue: k-tiles 0 and 1 in flight, k-tile 0 landed, its first-k-step fragments read
   set_load_tile(0);
@@ -1622,6 +1626,7 @@ void pp_tile(const comet_gemm_args& a, int& tbm, int& tbn) {
 // spanning the row. Instances: 128 x 384 / 64 x 384 (N = 384), 128 x 256 (N = 256).
 int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, a.alpha, COMET_ACT_NONE, 1};
+  e.prio = getenv("COMET_GEMM_PRIO") != nullptr;
   int grid = num_cus();
   grid -= grid % 8;
   int tbm, tbn;
@@ -1649,6 +1654,7 @@ template <typename TC>
 int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
   e.wide = (uintptr_t)a.c % 16 == 0 && a.ldc % 8 == 0 && getenv("COMET_GEMM_NO_WIDE") == nullptr;
+  e.prio = getenv("COMET_GEMM_PRIO") != nullptr;
   const w4::RowLN noln{};
   // N = 384 (the tracker's hidden size): 128 x 384 tiles (each A row block read once);
   // otherwise 256 x 256

@@ -20,8 +20,8 @@ import ref_harness as H  # noqa: E402
 import bench  # noqa: E402
 from oracle import prng  # noqa: E402
 
-MODES = ("train_fp32", "train_bf16", "eval_fp32")
-PROBE_S = {"train_fp32": 19.2, "train_bf16": 12.3, "eval_fp32": 14.6}  # SURVEY 6 / 8(d) probes, 8 cores
+MODES = ("train_bf16", "train_fp32", "eval_fp32", "eval_bf16")
+PROBE_S = {"train_fp32": 19.2, "train_bf16": 12.3, "eval_fp32": 14.6, "eval_bf16": None}  # SURVEY 6 / 8(d), 8 cores
 
 
 def reference_timer(T, S, N):
@@ -41,6 +41,7 @@ def reference_timer(T, S, N):
     def run(mode):
         kind, prec = mode.split("_")
         ctx = torch.autocast("cpu", dtype=torch.bfloat16) if prec == "bf16" else torch.autocast("cpu", enabled=False)
+        torch.autograd.set_detect_anomaly(False)  # camera_predictor10.py:305 turns it on inside the forward
         t0 = time.perf_counter()
         with ctx:
             if kind == "train":
@@ -73,7 +74,7 @@ def main():
         r, o = sum(d["reference"]) / 2, sum(d["oracle"]) / 2
         d["oracle_over_reference"] = round(o / r, 3)
         d["survey_probe_s"] = PROBE_S[mode]
-        d["reference_over_probe"] = round(r / PROBE_S[mode], 3)
+        d["reference_over_probe"] = round(r / PROBE_S[mode], 3) if PROBE_S[mode] else None
     print(json.dumps(rec, indent=1))
 
 

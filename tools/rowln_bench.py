@@ -54,8 +54,15 @@ def main():
                 ops.layernorm(c, eps=1e-6, out_dtype=torch.float32, dual=True)
 
         tf, ts = timed(fused), timed(separate)
-        print(f"M{M} N{N} K{K} {mode:9s} fused {tf:7.1f} us   gemm+LN {ts:7.1f} us   saved {ts - tf:6.1f} us "
-              f"({2 * M * N * K / tf / 1e6:.0f} TF/s fused)", flush=True)
+        nbytes = 2 * M * K + 2 * N * K + 4 * M * N * 2 + 2 * M * N * (1 + (z is not None))
+        extra = ""
+        if os.environ.get("COMET_ROWLN_AB"):  # B arm: the env var COMET_ROWLN_AB names, set to 1
+            os.environ[os.environ["COMET_ROWLN_AB"]] = "1"
+            tb = timed(fused)
+            del os.environ[os.environ["COMET_ROWLN_AB"]]
+            extra = f"   {os.environ['COMET_ROWLN_AB']}: {tb:7.1f} us ({nbytes / tb / 1e6:.2f} TB/s)"
+        print(f"M{M} N{N} K{K} {mode:9s} fused {tf:7.1f} us ({nbytes / tf / 1e6:.2f} TB/s, "
+              f"{2 * M * N * K / tf / 1e6:.0f} TF/s)   gemm+LN {ts:7.1f} us{extra}", flush=True)
 
 
 if __name__ == "__main__":
