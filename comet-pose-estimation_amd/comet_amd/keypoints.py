@@ -20,8 +20,10 @@ Here:
   * SIFT: LightGlue's SIFT wraps OpenCV / pycolmap, neither of which exists here; `sift=None`
     uses the SuperPoint keypoints alone.
 Parity: the NMS and filter_and_pad are pinned to fixtures generated from the reference tree
-(glue-factory's batched_nms = LightGlue's simple_nms; the reference's filter_and_pad); the network
-itself is unpinned (LightGlue and its weights are not in the reference tree).
+(glue-factory's batched_nms = LightGlue's simple_nms; the reference's filter_and_pad), and the
+network + keypoint selection to the reference tree's copy of the same magicleap network
+(gluefactory_nonfree/superpoint.py) run with PRNG weights (the trained superpoint_v1.pth is a
+download that is not available here); SIFT stays unpinned (absent).
 """
 import torch
 import torch.nn as nn
@@ -108,15 +110,20 @@ class SuperPoint(nn.Module):
                 "comet_maxpool2_nhwc")
         return y
 
-    def dense_scores(self, x):
-        """Preprocessed NHWC image [B, H, W, 8] -> keypoint scores [B, H', W'] after the NMS and the
-        border removal (LightGlue SuperPoint.forward up to the candidate selection)."""
+    def dense_probs(self, x):
+        """Preprocessed NHWC image [B, H, W, 8] -> dense keypoint probabilities [B, H, W] (encoder,
+        detector head, softmax with the dustbin dropped, depth-to-space; superpoint.py:202-233)."""
         for a, b in (("conv1a", "conv1b"), ("conv2a", "conv2b"), ("conv3a", "conv3b")):
             x = self._conv(self._conv(x, getattr(self, a)), getattr(self, b))
             x = self._pool(x)
         x = self._conv(self._conv(x, self.conv4a), self.conv4b)
         logits = self._conv(self._conv(x, self.convPa), self.convPb, relu=False, out_dtype=torch.float32)
-        scores = simple_nms(sp_scores(logits), self.conf["nms_radius"])
+        return sp_scores(logits)
+
+    def dense_scores(self, x):
+        """Preprocessed NHWC image [B, H, W, 8] -> keypoint scores [B, H', W'] after the NMS and the
+        border removal (LightGlue SuperPoint.forward up to the candidate selection)."""
+        scores = simple_nms(self.dense_probs(x), self.conf["nms_radius"])
         pad = self.conf["remove_borders"]
         if pad:
             scores[:, :pad] = -1

@@ -2125,8 +2125,8 @@ int launch_conv_skinny(const comet_conv_args& a, int64_t M, int OH, int OW, int 
 // conflict-free) in LDS, and walks a contiguous range of output rows: each output row needs one new
 // input row (prefetched into registers before the row's MFMAs, written to the ring after them),
 // so the input is read from HBM once instead of being gathered 9 times per tap from L2. Per row,
-// Cᵀ[cout][px] = W·Xᵀ on 32x32x16 MFMAs: wave w owns pixels 32w..32w+31 and all 64 outputs
-// (2 accumulators; 1.5 LDS fragment reads per MFMA), 36 k-steps (9 taps x 64 channels).
+// Cᵀ[cout][px] = W·Xᵀ on 32x32x16 MFMAs: 8 waves (2 per SIMD, so one hides the other's LDS latency)
+// each own 32 pixels x 32 outputs, 36 k-steps (9 taps x 64 channels).
 namespace cr {
 constexpr int CI = 64, CO = 64, KK = 9 * CI;  // channels, outputs, k
 constexpr int WP = KK + 8;                     // weight row pitch (elements)
@@ -2136,30 +2136,32 @@ constexpr int RP = (MAXW + 2) * PXP;           // ring row (elements)
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 template <typename TC>
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(512, 1)
 conv3_rows_kernel(const __bf16* __restrict__ x, int h, int w, const __bf16* __restrict__ wt, int64_t ldw,
                   TC* __restrict__ y, int64_t ldy, int64_t rows_total, int rows_per, Epi epi) {
   extern __shared__ __attribute__((aligned(16))) __bf16 lds[];
   __bf16* Ws = lds;                 // [CO][WP]
   __bf16* Xr = lds + CO * WP;       // [4][RP]
+  constexpr int NT = 512;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
+  const int pb = wid & 3, cb = wid >> 2;  // wave: pixels 32 pb.., outputs 32 cb..
   const int64_t R0 = (int64_t)blockIdx.x * rows_per;
   const int64_t R1 = R0 + rows_per < rows_total ? R0 + rows_per : rows_total;
   if (R0 >= R1) return;
 
   // weights (once) and the ring's pad columns (pixel 0 and w + 1 of every slot: zero forever)
-  for (int i = tid; i < CO * (KK / 8); i += 256) {
+  for (int i = tid; i < CO * (KK / 8); i += NT) {
     const int co = i / (KK / 8), c = i % (KK / 8);
     *reinterpret_cast<uint4*>(Ws + co * WP + 8 * c) = *reinterpret_cast<const uint4*>(wt + (int64_t)co * ldw + 8 * c);
   }
-  for (int i = tid; i < 4 * 2 * (CI / 8); i += 256) {
+  for (int i = tid; i < 4 * 2 * (CI / 8); i += NT) {
     const int slot = i / (2 * (CI / 8)), rem = i % (2 * (CI / 8));
     const int px = (rem / (CI / 8)) ? w + 1 : 0;
     *reinterpret_cast<uint4*>(Xr + slot * RP + px * PXP + 8 * (rem % (CI / 8))) = uint4{0, 0, 0, 0};
   }
   const int nch = w * (CI / 8);  // 16-B chunks of one input row
-  constexpr int MAXCH = MAXW * (CI / 8) / 256;  // per thread
+  constexpr int MAXCH = MAXW * (CI / 8) / NT;  // per thread
   uint4 st[MAXCH];
   // input row `row` (may be -1 or h: zeros) of image ni -> registers
   auto rload = [&](int64_t ni, int row) {
@@ -2167,7 +2169,7 @@ conv3_rows_kernel(const __bf16* __restrict__ x, int h, int w, const __bf16* __re
     const __bf16* src = x + ((ni * h + (in ? row : 0)) * (int64_t)w) * CI;
 #pragma unroll
     for (int i = 0; i < MAXCH; ++i) {
-      const int idx = tid + i * 256;
+      const int idx = tid + i * NT;
       st[i] = (in && idx < nch) ? *reinterpret_cast<const uint4*>(src + (int64_t)idx * 8) : uint4{0, 0, 0, 0};
     }
   };
@@ -2175,12 +2177,13 @@ conv3_rows_kernel(const __bf16* __restrict__ x, int h, int w, const __bf16* __re
     __bf16* dst = Xr + ((row + 1) & 3) * RP;
 #pragma unroll
     for (int i = 0; i < MAXCH; ++i) {
-      const int idx = tid + i * 256;
+      const int idx = tid + i * NT;
       if (idx < nch) *reinterpret_cast<uint4*>(dst + ((idx >> 3) + 1) * PXP + 8 * (idx & 7)) = st[i];
     }
   };
-  const int px = wid * 32 + r;  // this lane's output pixel (B operand column / output row)
+  const int px = pb * 32 + r;  // this lane's output pixel (B operand column / output row)
   const bool pxok = px < w;
+  const __bf16* wbase = Ws + (cb * 32 + r) * WP + 8 * hh;
 
   int64_t ni = R0 / h;
   int oy = (int)(R0 % h);
@@ -2192,58 +2195,51 @@ conv3_rows_kernel(const __bf16* __restrict__ x, int h, int w, const __bf16* __re
   for (int64_t R = R0; R < R1; ++R) {
     const bool next_same = R + 1 < R1 && oy + 1 < h;
     if (next_same) rload(ni, oy + 2);
-    f32x16 acc[2] = {f32x16{}, f32x16{}};
+    f32x16 acc = f32x16{};
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      const __bf16* xrow = Xr + ((oy + ky) & 3) * RP;
+      const __bf16* xb = Xr + ((oy + ky) & 3) * RP + px * PXP + 8 * hh;
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const __bf16* xb = xrow + (px + kx) * PXP + 8 * hh;
-        const __bf16* wb = Ws + r * WP + (ky * 3 + kx) * CI + 8 * hh;
+      for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
         for (int c = 0; c < CI; c += 16) {
-          const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xb + c);
-          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(wb + c);
-          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(wb + 32 * WP + c);
-          acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bx, acc[0], 0, 0, 0);
-          acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bx, acc[1], 0, 0, 0);
+          const bf16x8 bx = *reinterpret_cast<const bf16x8*>(xb + kx * PXP + c);
+          const bf16x8 aw = *reinterpret_cast<const bf16x8*>(wbase + (ky * 3 + kx) * CI + c);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw, bx, acc, 0, 0, 0);
         }
-      }
     }
     // epilogue: lane holds couts 32 cb + 8u + 4hh + (0..3) of pixel px; f32 values of the (u, u + 1)
     // pair are exchanged with the partner half so each lane owns 8 consecutive couts
     TC* yrow = y + (R * w + px) * ldy;
     const TC* rrow = reinterpret_cast<const TC*>(epi.resid) + (R * w + px) * epi.ldr;
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb)
+    for (int u = 0; u < 4; u += 2) {
+      float v[2][4];
 #pragma unroll
-      for (int u = 0; u < 4; u += 2) {
-        float v[2][4];
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int co = 32 * cb + 8 * (u + e) + 4 * hh + q;
-            v[e][q] = apply_act(epi.act, acc[cb][4 * (u + e) + q] + (epi.bias ? epi.bias[co] : 0.f));
-          }
-        float o[8];
+      for (int e = 0; e < 2; ++e)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][q]), __float_as_uint(v[1][q]), false, false);
-          o[q] = __uint_as_float(sw[0]);
-          o[4 + q] = __uint_as_float(sw[1]);
+          const int co = 32 * cb + 8 * (u + e) + 4 * hh + q;
+          v[e][q] = apply_act(epi.act, acc[4 * (u + e) + q] + (epi.bias ? epi.bias[co] : 0.f));
         }
-        const int co0 = 32 * cb + 8 * u + 8 * hh;
-        if (pxok) {
-          if (epi.resid) {
-            float rv[8];
-            load8(rrow + co0, rv);
+      float o[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) o[q] += epi.beta * rv[q];
-          }
-          store8(yrow + co0, o);
-        }
+      for (int q = 0; q < 4; ++q) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][q]), __float_as_uint(v[1][q]), false, false);
+        o[q] = __uint_as_float(sw[0]);
+        o[4 + q] = __uint_as_float(sw[1]);
       }
+      const int co0 = 32 * cb + 8 * u + 8 * hh;
+      if (pxok) {
+        if (epi.resid) {
+          float rv[8];
+          load8(rrow + co0, rv);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] += epi.beta * rv[q];
+        }
+        store8(yrow + co0, o);
+      }
+    }
     if (next_same) rstore(oy + 2);
     __syncthreads();  // ring slot of row oy - 1 (refilled above) and this row's reads are done
     ++oy;
@@ -2265,7 +2261,8 @@ template <typename TC>
 bool conv_rows_ok(const comet_conv_args& a) {
   if (getenv("COMET_CONV_NO_ROWS") != nullptr) return false;
   if (a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1 || a.c != cr::CI || a.cout != cr::CO) return false;
-  if (a.w > cr::MAXW || a.w % 32 != 0 || a.ldw < cr::KK || a.ldw % 8 != 0 || a.n * a.h < 256) return false;
+  // w >= 96: all four waves own pixels (at w = 64 the implicit GEMM is faster, tools/conv_bench.py)
+  if (a.w > cr::MAXW || a.w < 96 || a.w % 32 != 0 || a.ldw < cr::KK || a.ldw % 8 != 0 || a.n * a.h < 256) return false;
   const uintptr_t al = 8 * sizeof(TC) >= 16 ? 16 : 8 * sizeof(TC);
   if ((uintptr_t)a.y % al != 0 || a.ldy % 8 != 0) return false;
   if (a.resid && ((uintptr_t)a.resid % al != 0 || a.ldr % 8 != 0)) return false;
@@ -2285,7 +2282,7 @@ int launch_conv_rows(const comet_conv_args& a, hipStream_t s) {
     (void)hipFuncSetAttribute((const void*)cr::conv3_rows_kernel<TC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  hipLaunchKernelGGL((cr::conv3_rows_kernel<TC>), dim3((unsigned)grid), dim3(256), lds, s, (const __bf16*)a.x,
+  hipLaunchKernelGGL((cr::conv3_rows_kernel<TC>), dim3((unsigned)grid), dim3(512), lds, s, (const __bf16*)a.x,
                      (int)a.h, (int)a.w, (const __bf16*)a.weight, a.ldw, (TC*)a.y, a.ldy, rows, rows_per, e);
   COMET_CHECK_LAUNCH("comet_conv2d_nhwc (3x3 rows in LDS)");
   return COMET_OK;

@@ -1,8 +1,9 @@
 """SURVEY §8(f1) keypoint initialisation on the GPU: the SuperPoint NMS (comet_maxfilt2d) and
 filter_and_pad vs fixtures from the reference tree (tests/golden/comet_golden_kp.npz), the
-detector-head decode / max pooling / preprocessing kernels vs torch fp32 references, and an
-extract() + keypoint_tracks run (random weights: LightGlue's superpoint_v1.pth is not available
-offline, so detections are unpinned -- checked for shape, range and count)."""
+detector-head decode / max pooling / preprocessing kernels vs torch fp32 references, the SuperPoint
+network + keypoint selection vs the reference tree's gluefactory_nonfree/superpoint.py run with PRNG
+weights (tools/gen_golden.py --keypoints; the trained superpoint_v1.pth is not available offline),
+and an extract() + keypoint_tracks run."""
 import os
 
 import numpy as np
@@ -117,3 +118,59 @@ def test_superpoint_extract_and_tracks(dtype):
         mask = torch.ones(2, 128, 160, dtype=torch.bool, device="cuda")
         tracks, vis = keypoint_tracks(sp, imgs, mask, track_num=64, min_required=64)
         assert tracks.shape == (2, 4, 64, 2) and vis.shape == (2, 4, 64) and bool(vis.all())
+
+
+def _sp_prng(seed, K):
+    """SuperPoint with the fixture's PRNG weights (tools/gen_golden.py gen_superpoint_net: fan-in
+    uniform, encoder x2, detector head x40)."""
+    from comet_amd.keypoints import SuperPoint
+    from oracle import prng
+    sp = SuperPoint(max_num_keypoints=K, detection_threshold=0.005, resize=None)
+    shapes = {k: tuple(v.shape) for k, v in sp.state_dict().items()}
+    sd = dict(prng.make_state_dict(seed, shapes))
+    for k in sd:
+        if k.endswith(".weight"):
+            sd[k] = sd[k] * (40.0 if k.startswith("convPb") else 2.0)
+    sp.load_state_dict(sd, strict=True)
+    return sp.cuda().eval()
+
+
+def test_superpoint_network_matches_reference(gold):
+    """fp32: dense probabilities within 1e-5 relative of the reference network's, and the same top-K
+    keypoints (pixel positions exactly, in the same score order) with the same scores."""
+    from comet_amd import functional as F
+    seed, K = (int(v) for v in gold["spn_cfg"])
+    sp = _sp_prng(seed, K)
+    for t in "abc":
+        img = torch.from_numpy(gold[f"spn{t}_img"]).cuda()
+        Hh, Ww = img.shape[-2:]
+        with F.precision(torch.float32):
+            prob = sp.dense_probs(sp._preprocess(img, Hh, Ww))
+            out = sp.extract(img[0])
+        ref = torch.from_numpy(gold[f"spn{t}_prob"])
+        err = ((prob.cpu() - ref).abs() / ref.abs().clamp_min(1e-6)).max().item()
+        print(f"{t}: dense probability max rel err {err:.2e}")
+        assert err < 1e-4
+        np.testing.assert_array_equal(out["keypoints"].cpu().numpy(), gold[f"spn{t}_kp"])
+        np.testing.assert_allclose(out["keypoint_scores"].cpu().numpy(), gold[f"spn{t}_kps"], rtol=1e-4)
+
+
+def test_superpoint_network_bf16_selects_the_same_keypoints(gold):
+    """bf16 (the training loop's precision): probabilities within 2e-2 relative; the top-K sets agree
+    except where two reference scores sit within bf16 noise of each other at the cut."""
+    from comet_amd import functional as F
+    seed, K = (int(v) for v in gold["spn_cfg"])
+    sp = _sp_prng(seed, K)
+    for t in "abc":
+        img = torch.from_numpy(gold[f"spn{t}_img"]).cuda()
+        Hh, Ww = img.shape[-2:]
+        with F.precision(torch.bfloat16):
+            prob = sp.dense_probs(sp._preprocess(img, Hh, Ww))
+            out = sp.extract(img[0])
+        ref = torch.from_numpy(gold[f"spn{t}_prob"])
+        err = ((prob.float().cpu() - ref).abs() / ref.abs().clamp_min(1e-6)).max().item()
+        got = {tuple(p) for p in out["keypoints"][0].cpu().numpy().tolist()}
+        exp = {tuple(p) for p in gold[f"spn{t}_kp"][0].tolist()}
+        print(f"{t}: bf16 probability max rel err {err:.2e}, keypoints in common {len(got & exp)} / {K}")
+        assert err < 2e-2
+        assert len(got & exp) >= K - 4

@@ -712,10 +712,86 @@ def gen_keypoints(out):
         print("filter_and_pad", tag, tuple(kept.shape))
 
 
+SP_NET = os.path.join(H.REF, "comet", "models", "dependency", "glue-factory", "gluefactory_nonfree", "superpoint.py")
+
+
+def gen_superpoint_net(out, seed=7, K=64):
+    """The SuperPoint network (magicleap superpoint_v1 architecture, the reference tree's
+    gluefactory_nonfree/superpoint.py:152-350, which is the network LightGlue's SuperPoint wraps)
+    with PRNG weights (oracle/prng.py, seed `seed`) on three RGB images at identity resize: the
+    dense keypoint probabilities (softmax, dustbin dropped, depth-to-space) and the sparse output
+    (simple_nms r=4, 4-px borders, threshold 0.005, top-K). Only the config plumbing of glue-factory's
+    BaseModel is stubbed (OmegaConf is not installed): the network and the keypoint selection run
+    as the reference file defines them; torch.hub's checkpoint download returns the PRNG state dict."""
+    import importlib.util
+    import types
+    H.install_stubs()
+
+    class _Conf(dict):
+        __getattr__ = dict.__getitem__
+
+    class _BaseModel(torch.nn.Module):  # glue-factory BaseModel's conf merge, without OmegaConf
+        default_conf = {}
+
+        def __init__(self, conf):
+            super().__init__()
+            self.conf = _Conf({**type(self).default_conf, **conf})
+            self._init(self.conf)
+
+        def forward(self, data):
+            return self._forward(data)
+
+    for name in ("gluefactory", "gluefactory.models", "gluefactory.models.utils"):
+        mod = types.ModuleType(name)
+        mod.__path__ = []
+        sys.modules.setdefault(name, mod)
+    sys.modules["gluefactory.models.base_model"] = types.SimpleNamespace(BaseModel=_BaseModel)
+    sys.modules["gluefactory.models.utils.misc"] = types.SimpleNamespace(pad_and_stack=None)
+    spec = importlib.util.spec_from_file_location("gluefactory_nonfree.superpoint", SP_NET)
+    sp_mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sp_mod)
+    shapes = {}
+    c = {"conv1a": (64, 1, 3), "conv1b": (64, 64, 3), "conv2a": (64, 64, 3), "conv2b": (64, 64, 3),
+         "conv3a": (128, 64, 3), "conv3b": (128, 128, 3), "conv4a": (128, 128, 3), "conv4b": (128, 128, 3),
+         "convPa": (256, 128, 3), "convPb": (65, 256, 1), "convDa": (256, 128, 3), "convDb": (256, 256, 1)}
+    for n, (co, ci, k) in c.items():
+        shapes[n + ".weight"] = (co, ci, k, k)
+        shapes[n + ".bias"] = (co,)
+    sd = dict(prng.make_state_dict(seed, shapes))
+    # fan-in-scaled PRNG weights leave the 65 detector logits within ~1e-3 of each other (near-uniform
+    # softmax, top-k decided by float ties): the detector head and the encoder are scaled up so the
+    # scores spread over orders of magnitude and the selection is well conditioned
+    for n in c:
+        sd[n + ".weight"] = sd[n + ".weight"] * (40.0 if n == "convPb" else 2.0)
+    orig = torch.hub.load_state_dict_from_url
+    torch.hub.load_state_dict_from_url = lambda *a, **k: sd
+    try:
+        dense = sp_mod.SuperPoint({"sparse_outputs": False, "has_descriptor": True}).eval()
+        sparse = sp_mod.SuperPoint({"max_num_keypoints": K, "detection_threshold": 0.005}).eval()
+    finally:
+        torch.hub.load_state_dict_from_url = orig
+    g = torch.Generator().manual_seed(seed + 1)
+    for tag, (Hh, Ww) in {"a": (64, 96), "b": (80, 80), "c": (48, 120)}.items():
+        img = torch.rand(1, 3, Hh // 4, Ww // 4, generator=g)
+        img = torch.nn.functional.interpolate(img, size=(Hh, Ww), mode="bilinear", align_corners=False)
+        img = (img + 0.05 * torch.rand(1, 3, Hh, Ww, generator=g)).clamp(0, 1)  # smooth structure + texture
+        with torch.no_grad():
+            pd = dense({"image": img})
+            ps = sparse({"image": img})
+        out[f"spn{tag}_img"] = img.numpy()
+        out[f"spn{tag}_prob"] = pd["keypoint_scores"].numpy()
+        # glue-factory returns pixel (x, y) + 0.5; LightGlue (the reference loop's extractor) the pixel
+        out[f"spn{tag}_kp"] = (ps["keypoints"] - 0.5).numpy()
+        out[f"spn{tag}_kps"] = ps["keypoint_scores"].numpy()
+        print("superpoint", tag, tuple(ps["keypoints"].shape))
+    out["spn_cfg"] = np.array([seed, K])
+
+
 def main_keypoints():
     H.require_reference()
     out = {}
     gen_keypoints(out)
+    gen_superpoint_net(out)
     path = os.path.join(OUT, "comet_golden_kp.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
