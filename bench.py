@@ -45,7 +45,7 @@ def parse():
                     help="BASELINE configs[1]: full COMET forward only (eval, no_grad), no loss backward / optimizer")
     ap.add_argument("--cpu-baseline-only", action="store_true")
     ap.add_argument("--cpu-baseline-quick", action="store_true",
-                    help="CPU baseline of train bf16 only, 1 rep (default: every SURVEY 8(d) mode, 2 reps each)")
+                    help="CPU baseline of train fp32 only, 1 rep (default: every SURVEY 8(d) mode, 2 reps each)")
     ap.add_argument("--launcher-check", action="store_true",
                     help="CPU self-test of the --gpus N launcher: gloo ranks, one bucketed gradient all-reduce, no GPU")
     return ap.parse_args()
@@ -139,8 +139,8 @@ def synthetic(B, T, S_img, N, device, seed):
 
 
 CPU_MODES = {
-    "train_bf16": "train step fwd+bwd+clip+AdamW, bf16 autocast",
     "train_fp32": "train step fwd+bwd+clip+AdamW, fp32",
+    "train_bf16": "train step fwd+bwd+clip+AdamW, bf16 autocast",
     "eval_fp32": "eval forward (no_grad), fp32",
     "eval_bf16": "eval forward (no_grad), bf16 autocast",
 }
@@ -206,9 +206,11 @@ def oracle_timer(T, S_img, N):
 def cpu_baseline(T, S_img, N, modes=tuple(CPU_MODES), reps=2, warmup_frames=4):
     """The oracle timed on this host's cores: per mode one warm-up (a T=`warmup_frames`
     sequence: thread pool, allocator and first-call costs, bounded) then `reps` timed sequences at
-    the full size; value = 1 / mean seconds of the first mode (train bf16: the precision of the GPU
-    line). Default: every 8(d) mode (train / eval x fp32 / bf16), 2 reps each (~2 min of CPU);
-    `--cpu-baseline-quick` times train bf16 once."""
+    the full size; value = 1 / mean seconds of the first mode, train fp32: the mode in which the
+    restatement times within 3 % of the reference itself (profiles/r03_cpu_calibration.json; its bf16
+    autocast modes run 1.7-1.9x faster than the reference's, so they would flatter neither side
+    honestly). Default: every 8(d) mode (train / eval x fp32 / bf16), 2 reps each (~2 min of CPU);
+    `--cpu-baseline-quick` times train fp32 once."""
     threads = cpu_threads()
     torch.set_num_threads(threads)
     print(f"[bench] cpu baseline: oracle {list(modes)} on {threads} threads ...", file=sys.stderr, flush=True)
@@ -250,7 +252,7 @@ def pmc_traffic(instance, config):
 
 def main():
     args = parse()
-    cpu_modes = ("train_bf16",) if args.cpu_baseline_quick else tuple(CPU_MODES)
+    cpu_modes = ("train_fp32",) if args.cpu_baseline_quick else tuple(CPU_MODES)
     cpu_reps = 1 if args.cpu_baseline_quick else 2
     if args.cpu_baseline_only:
         print(json.dumps(cpu_baseline(args.frames, args.image, args.tracks, modes=cpu_modes, reps=cpu_reps)))
