@@ -110,6 +110,7 @@ class SuperPoint(nn.Module):
                 "comet_maxpool2_nhwc")
         return y
 
+    @torch.no_grad()
     def dense_probs(self, x):
         """Preprocessed NHWC image [B, H, W, 8] -> dense keypoint probabilities [B, H, W] (encoder,
         detector head, softmax with the dustbin dropped, depth-to-space; superpoint.py:202-233)."""
@@ -120,6 +121,7 @@ class SuperPoint(nn.Module):
         logits = self._conv(self._conv(x, self.convPa), self.convPb, relu=False, out_dtype=torch.float32)
         return sp_scores(logits)
 
+    @torch.no_grad()
     def dense_scores(self, x):
         """Preprocessed NHWC image [B, H, W, 8] -> keypoint scores [B, H', W'] after the NMS and the
         border removal (LightGlue SuperPoint.forward up to the candidate selection)."""
