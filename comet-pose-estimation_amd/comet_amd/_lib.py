@@ -6,7 +6,10 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("COMET_HIP_LIB", os.path.join(os.path.dirname(_HERE), "libcomet_hip.so"))
+# COMET_DEBUG=1 selects the `make DEBUG=1` library (a synchronise + device index-check read after
+# every launch; comet_amd/debug.py); COMET_HIP_LIB names any other build explicitly
+_DEFAULT_LIB = "libcomet_hip_debug.so" if os.environ.get("COMET_DEBUG") == "1" else "libcomet_hip.so"
+LIB_PATH = os.environ.get("COMET_HIP_LIB", os.path.join(os.path.dirname(_HERE), _DEFAULT_LIB))
 
 F32 = 0
 BF16 = 1
@@ -87,6 +90,8 @@ class AttnBwdArgs(ctypes.Structure):
 _F = ctypes.c_float
 _INT = ctypes.c_int
 SIGNATURES = {
+    "comet_count_nonfinite": (_INT, [_INT, c_vp, c_i64, c_vp, c_vp]),
+    "comet_debug_flags": (_INT, [_INT]),
     "comet_version": (_INT, []),
     "comet_last_error": (ctypes.c_char_p, []),
     "comet_gemm": (_INT, [ctypes.POINTER(GemmArgs), c_vp]),

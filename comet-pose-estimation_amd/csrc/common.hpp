@@ -23,6 +23,35 @@ void set_error(const std::string& msg);
     }                                       \
   } while (0)
 
+#ifdef COMET_DEBUG
+// debug build: synchronise after every launch (a fault is attributed to the op that caused it) and
+// read this translation unit's device assertion word, which the kernels' COMET_DASSERT checks set
+static __device__ int g_dbg_word = 0;  // (inside namespace comet)
+void debug_record(const char* name, int word);
+#define COMET_CHECK_LAUNCH(name)                                                              \
+  do {                                                                                        \
+    hipError_t e_ = hipGetLastError();                                                        \
+    if (e_ == hipSuccess) e_ = hipDeviceSynchronize();                                        \
+    if (e_ != hipSuccess) {                                                                   \
+      ::comet::set_error(std::string(name) + ": " + hipGetErrorString(e_));                   \
+      return COMET_ELAUNCH;                                                                   \
+    }                                                                                         \
+    int w_ = 0;                                                                               \
+    (void)hipMemcpyFromSymbol(&w_, HIP_SYMBOL(::comet::g_dbg_word), sizeof(int));             \
+    if (w_ != 0) {                                                                            \
+      const int z_ = 0;                                                                       \
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(::comet::g_dbg_word), &z_, sizeof(int));             \
+      ::comet::debug_record(name, w_);                                                        \
+      return COMET_ELAUNCH;                                                                   \
+    }                                                                                         \
+  } while (0)
+// a failed check records its source line (mod 31) in the word -- no trap: a faulting wave can take
+// the whole device down; the access the check guards still happens
+#define COMET_DASSERT(cond)                                                      \
+  do {                                                                           \
+    if (!(cond)) atomicOr(&::comet::g_dbg_word, 1 << (__LINE__ % 31));           \
+  } while (0)
+#else
 #define COMET_CHECK_LAUNCH(name)                                                 \
   do {                                                                           \
     hipError_t e_ = hipGetLastError();                                           \
@@ -31,6 +60,8 @@ void set_error(const std::string& msg);
       return COMET_ELAUNCH;                                                      \
     }                                                                            \
   } while (0)
+#define COMET_DASSERT(cond) do { } while (0)
+#endif
 
 // ---- scalar conversions -------------------------------------------------------------------
 __device__ __forceinline__ float to_f32(float x) { return x; }

@@ -432,3 +432,34 @@ extern "C" int comet_adamw_multi(float* const* params, const float* const* grads
   }
   return COMET_OK;
 }
+
+// ---- NaN / Inf census (debug support, comet_amd.debug) --------------------------------------
+namespace comet {
+namespace {
+template <typename T>
+__global__ void __launch_bounds__(256) nonfinite_kernel(const T* __restrict__ x, int64_t n, int32_t* __restrict__ count) {
+  int c = 0;
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    c += !isfinite(to_f32(x[i]));
+  c = (int)wave_sum((float)c);
+  if ((threadIdx.x & 63) == 0 && c != 0) atomicAdd(count, c);
+}
+}  // namespace
+}  // namespace comet
+
+extern "C" int comet_count_nonfinite(int dtype, const void* x, int64_t n, int32_t* count, void* stream) {
+  using namespace comet;
+  COMET_CHECK_ARG(x != nullptr && count != nullptr && n >= 0, "comet_count_nonfinite: bad args");
+  if (n == 0) return COMET_OK;
+  const unsigned g = (unsigned)(cdiv(n, 256) < 4096 ? cdiv(n, 256) : 4096);
+  if (dtype == COMET_BF16)
+    hipLaunchKernelGGL(nonfinite_kernel<__bf16>, dim3(g), dim3(256), 0, as_stream(stream), (const __bf16*)x, n, count);
+  else if (dtype == COMET_F32)
+    hipLaunchKernelGGL(nonfinite_kernel<float>, dim3(g), dim3(256), 0, as_stream(stream), (const float*)x, n, count);
+  else {
+    set_error("comet_count_nonfinite: bad dtype");
+    return COMET_EINVAL;
+  }
+  COMET_CHECK_LAUNCH("comet_count_nonfinite");
+  return COMET_OK;
+}

@@ -2174,6 +2174,7 @@ conv3_rows_kernel(const __bf16* __restrict__ x, int h, int w, const __bf16* __re
     }
   };
   auto rstore = [&](int row) {
+    COMET_DASSERT(row >= -1 && row <= h);  // the ring holds rows -1 .. h (zero pad rows included)
     __bf16* dst = Xr + ((row + 1) & 3) * RP;
 #pragma unroll
     for (int i = 0; i < MAXCH; ++i) {

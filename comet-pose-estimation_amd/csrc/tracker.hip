@@ -291,6 +291,9 @@ __global__ void patch_gather_kernel(const float* __restrict__ images, const floa
     const int x0 = tlx < 0 ? 0 : (tlx > lim ? lim : tlx);
     const int y0 = tly < 0 ? 0 : (tly > lim ? lim : tly);
     const int64_t bs = t / N;
+    // the patch must lie inside the frame: the reference's H-for-both-axes clamp needs W >= H, and
+    // a NaN track coordinate has no defined floor
+    COMET_DASSERT(x0 >= 0 && x0 + P <= W && y0 >= 0 && y0 + P <= H && cx == cx && cy == cy);
     const int64_t pix = (int64_t)(y0 + py) * W + (x0 + px), plane = (int64_t)H * W;
     const float* src = images + bs * 3 * plane + pix;
     TO* dst = patches + q * cpad;

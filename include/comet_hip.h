@@ -438,6 +438,18 @@ int comet_maxpool2_nhwc(int dtype, const void* x, void* y, int64_t n, int H, int
 int comet_sp_scores(const float* logits, float* scores, int B, int h, int w, void* stream);
 int comet_maxfilt2d(const float* x, float* y, float* tmp, int B, int H, int W, int r, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Debug support (bounds asserts and a NaN / Inf check mode).
+ * comet_count_nonfinite: adds the number of NaN / Inf elements of x (n elements, dtype) to
+ *   *count (an int32 on the device; no host sync). Used by comet_amd.debug's finite-check hooks.
+ * comet_debug_flags: the build's debug state. In a `make DEBUG=1` library (libcomet_hip_debug.so,
+ *   compiled with COMET_DEBUG) every launch is followed by a device synchronise and a read of the
+ *   device-side assertion word (index checks inside the kernels record a failed check there instead
+ *   of trapping); the call returns that word and clears it (clear != 0). A release library returns
+ *   -1. */
+int comet_count_nonfinite(int dtype, const void* x, int64_t n, int32_t* count, void* stream);
+int comet_debug_flags(int clear);
+
 #ifdef __cplusplus
 }
 #endif
