@@ -60,8 +60,8 @@ def test_finite_check_names_the_module_and_the_gradient():
     from comet_amd._lib import CometHipError
     from comet_amd.models.modules import AttnBlock
     torch.manual_seed(0)
-    blk = AttnBlock(96, 4).cuda()
-    x = torch.randn(2, 20, 96, device="cuda")
+    blk = AttnBlock(128, 4).cuda()
+    x = torch.randn(2, 20, 128, device="cuda")
     with F.precision(torch.float32), debug.FiniteCheck(blk):
         blk(x).sum().backward()  # finite: no error
     debug.check_grads(blk)
