@@ -42,7 +42,6 @@ struct Epi {
   int vec;  // output / resid / aux rows allow 8-wide vector access (host-checked)
   int wide = 0;  // persistent kernel: 16-B bf16 stores (C 16-B aligned, ldc % 8 == 0; host-checked)
   int prio = 0;  // persistent kernel: s_setprio 1 for waves 4-7 (COMET_GEMM_PRIO=1, measurement)
-  int rdma = 0;  // persistent kernel: f32 residual by LDS-DMA (R 16-B aligned rows; host-checked)
 };
 
 // Split-K partials: ws[((z * nb) + bz) * M * N + row * N + col], f32.
@@ -1034,16 +1033,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   auto pswz = [](int r) { return PSWZ ? ((r & 7) | ((r & 2) << 2)) : 0; };
   static_assert(!LN || (PARK && std::is_same<TC, float>::value), "row LN epilogue: parked f32 outputs only");
   constexpr int STATS_F = LN ? 2 * TBM * WN : 0;  // f32 row-partial table (sum, sum of squares)
-  // f32 residual of the parked epilogue: each 8-row half block's residual arrives by LDS-DMA into a
-  // per-wave buffer while the previous half block is stored (one 1-KiB piece per column pass; a lane
-  // reads back exactly the 16 B it fetched), instead of a register load whose HBM latency every half
-  // block waited out (SQ_WAIT_ANY 54-64 % of the wave time on the f32-residual shapes,
-  // profiles/r03_gpmc). Where the LDS allows it (the 256 x 256 tiles); COMET_GEMM_NO_RDMA=1 at
-  // launch selects the register loads.
-  constexpr int PNTC = WCOLS / (8 * (16 / (int)sizeof(TC)));
-  constexpr int RBUF_F = (PARK && HASR && !LN && std::is_same<TC, float>::value) ? NW * PNTC * 256 : 0;
-  constexpr bool RDMA = RBUF_F > 0 && (2 * BUF + 2 * PARK_F + 2 * STATS_F + 2 * RBUF_F) * 2 <= 163840;
-  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + 2 * PARK_F + 2 * STATS_F + (RDMA ? 2 * RBUF_F : 0)];
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + 2 * PARK_F + 2 * STATS_F];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / WN, wc = wid % WN;
@@ -1443,22 +1433,8 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       const int rr = lane >> 3, cc = lane & 7;
       const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;        // + i*16 + h*8
       const int64_t pcol0 = (int64_t)tn * TBN + wc * WCOLS + cc * CPL;  // + t*8*CPL
-      float* rbuf = reinterpret_cast<float*>(smem + 2 * BUF + 2 * PARK_F + 2 * STATS_F) + wid * PNTC * 256;
-      auto rdma = [&](int jj) {  // residual of half block jj = 2i + h -> rbuf (rows clamped: tails unused)
-        const int64_t rowj = min(prow0 + (jj >> 1) * 16 + (jj & 1) * 8, M - 1);
-#pragma unroll
-        for (int t = 0; t < NTC; ++t) {
-          const int64_t col = min(pcol0 + t * 8 * CPL, N - CPL);
-          __builtin_amdgcn_global_load_lds((const void*)(R + rowj * epi.ldr + col), (lds_void*)(rbuf + t * 256), 16, 0, 0);
-        }
-      };
       auto pepilogue = [&](auto edge_t) {
         constexpr bool EDGE = decltype(edge_t)::value;
-        const bool rd = RDMA && epi.rdma;
-        if constexpr (RDMA && HASR) {
-          if (rd) rdma(0);
-          asm volatile("" ::: "memory");
-        }
         const bool bias_c = epi.bias != nullptr;  // per-column bias only (pp_ok)
         float bcp[NTC][CPL];
 #pragma unroll
@@ -1483,26 +1459,10 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
             float rc[NTC][CPL];
             const int64_t row = prow0 + i * 16 + h * 8;
             if constexpr (HASR) {
-              if (RDMA && rd) {
-                // this half block's DMA was issued before the previous half block's NTC stores
-                // (or first, ahead of the bias loads): wait for it, read the lane's own 16 B back,
-                // then start the next half block's DMA into the freed buffer
-                if (EDGE || (i == 0 && h == 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NTC) : "memory");
 #pragma unroll
-                for (int t = 0; t < NTC; ++t) {
-                  const f32x4 r4 = *reinterpret_cast<const f32x4*>(rbuf + t * 256 + 4 * lane);
-                  rc[t][0] = r4[0]; rc[t][1] = r4[1]; rc[t][2] = r4[2]; rc[t][3] = r4[3];
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (2 * i + h + 1 < 2 * MI) rdma(2 * i + h + 1);
-                asm volatile("" ::: "memory");
-              } else {
-#pragma unroll
-                for (int t = 0; t < NTC; ++t) {
-                  const int64_t col = pcol0 + t * 8 * CPL;
-                  if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, rc[t]);
-                }
+              for (int t = 0; t < NTC; ++t) {
+                const int64_t col = pcol0 + t * 8 * CPL;
+                if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, rc[t]);
               }
             }
             if ((li >> 3) == h) {
@@ -1695,7 +1655,6 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
   e.wide = (uintptr_t)a.c % 16 == 0 && a.ldc % 8 == 0 && getenv("COMET_GEMM_NO_WIDE") == nullptr;
   e.prio = getenv("COMET_GEMM_PRIO") != nullptr;
-  e.rdma = a.resid != nullptr && (uintptr_t)a.resid % 16 == 0 && a.ldr % 4 == 0 && getenv("COMET_GEMM_NO_RDMA") == nullptr;
   const w4::RowLN noln{};
   // N = 384 (the tracker's hidden size): 128 x 384 tiles (each A row block read once);
   // otherwise 256 x 256
