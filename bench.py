@@ -233,6 +233,20 @@ def cpu_baseline(T, S_img, N, modes=tuple(CPU_MODES), reps=2, warmup_frames=4):
     return out
 
 
+def workload_label(fwd, B, T, image, world):
+    """Name the BASELINE.json config a run measures; anything else is labelled as a custom size."""
+    what = ("COMET fwd-only (tracker+DINOv2+head, pose loss, no backward)" if fwd else
+            "train_e2epose2.py fwd+bwd (COMET tracker+DINOv2+head, loss, backward, grad all-reduce, clip 1.0, AdamW)")
+    if (B, T, image) == (8, 16, 512):
+        tag = "BASELINE configs[1]" if fwd else ("BASELINE configs[3] (DDP, B=8 per GPU)" if world > 1 else
+                                                   "BASELINE configs[2]")
+    elif (B, T, image) == (4, 64, 768) and world == 1:
+        tag = "BASELINE configs[4] long-sequence stress"
+    else:
+        tag = f"custom size B={B} T={T} {image}^2 (not a BASELINE config)"
+    return f"{what} -- {tag}"
+
+
 def pmc_traffic(instance, config):
     """HBM bytes per launch of `instance` from the newest committed PMC summary
     (profiles/r*_pmc.json, tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE per dispatch, from
@@ -406,9 +420,7 @@ def main():
             "value": round(value, 4), "unit": "sequences/s", "n_gpus": dist.get_world_size() if world > 1 else 1, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic (N(0,1) frames, U[0,511] tracks, random unit quaternions); random-init weights",
-            "config": {"workload": ("COMET fwd-only eval (BASELINE configs[1]): tracker+DINOv2+head, pose loss, no backward" if fwd else
-                                    "train_e2epose2.py fwd+bwd (BASELINE configs[2]): COMET tracker+DINOv2+head, loss, backward, "
-                                    "grad all-reduce, clip 1.0, AdamW"), "global_batch": B * world, "seq_len": T,
+            "config": {"workload": workload_label(fwd, B, T, args.image, world), "global_batch": B * world, "seq_len": T,
                        "image": args.image, "tracks": args.tracks, "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "distributed": comm, "kernels": kernels, "kernel_instances": instances, "final_loss": float(loss.item()) if loss is not None else None,
             "ms_per_step_profiled": round(elapsed_prof / args.steps * 1e3, 2),
