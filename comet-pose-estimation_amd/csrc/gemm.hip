@@ -985,6 +985,22 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int SG_MFMA = 0x008, SG_DSR = 0x100, SG_VMR = 0x020;
 
+#ifdef COMET_GEMM_STAMPS
+// Diagnostic build only (make STAMPS=1 -> libcomet_hip_stamp.so): wave 0 of each workgroup records
+// the shader clock at the start of each tile's k-loop, before and after its epilogue; written by
+// lane 0 with a vector store into g_stamps[workgroup][tile][phase] (tools/gemm_stamps.py).
+constexpr int ST_WG = 256, ST_TILES = 64;
+__device__ unsigned long long g_stamps[ST_WG * ST_TILES * 4];
+__device__ __forceinline__ void stamp(int bid, int wid, int tile, int ph) {
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  if (wid == 0 && bid < ST_WG && tile < ST_TILES && (threadIdx.x & 63) == 0)
+    g_stamps[((bid * ST_TILES + tile) << 2) + ph + (threadIdx.x & 63)] = t;
+}
+#define COMET_STAMP(tile, ph) stamp(bid, wid, (tile), (ph))
+#else
+#define COMET_STAMP(tile, ph) ((void)0)
+#endif
+
 // Row LayerNorm fused into the f32 epilogue when one tile spans the whole output row (N == TBN:
 // the tracker's hidden sizes 384 / 256). With v = the epilogue value of a row (bias, residual):
 //   C   = v (raw_c) or (v - mean) * rstd(eps_y)                [f32: residual stream / dual copy]
@@ -1132,6 +1148,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   read_frags(0, 0, a0, b0);
 
   for (int q = 0; q < T; ++q) {
+    if (q % nk == 0) COMET_STAMP(q / nk, 0);
     // ---- k-step 0 of k-tile q: MFMAs on (a0, b0), reads of the k-step-1 fragments (a1, b1)
     read_frags(q & 1, 1, a1, b1);
     mfmas(a0, b0);
@@ -1189,6 +1206,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     advance();
 
     if (!tile_end) continue;
+    COMET_STAMP(q / nk, 1);
     // ---- epilogue of tile q / nk, straight from the accumulators: lane (li, g) of fragment
     // (i, j) holds C[row0 + i*16 + li][col0 + j*16 + 4g + r], r = 0..3
     int tm, tn;
@@ -1550,7 +1568,12 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // count is fixed, so the next barrier wait leaves them in flight
     if constexpr (WIDE) pend = (interior && X == nullptr && epi.wide) ? 1 : 0;
     else pend = interior ? 1 : 0;
+    COMET_STAMP(q / nk, 2);
   }
+#ifdef COMET_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  COMET_STAMP(my_tiles, 3);
+#endif
 }
 }  // namespace w4
 
@@ -2401,6 +2424,22 @@ extern "C" int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_a
               ln->zw, ln->zb, ln->eps_z, ln->raw_c};
   return launch_pp_rowln(*args, r, as_stream(stream));
 }
+
+#ifdef COMET_GEMM_STAMPS
+// diagnostic build: copy out / clear the per-tile clock stamps of the persistent GEMM
+extern "C" int comet_gemm_stamps(unsigned long long* host, int64_t n, int clear) {
+  using namespace comet;
+  const int64_t cap = (int64_t)w4::ST_WG * w4::ST_TILES * 4;
+  if (n > cap) n = cap;
+  if (host != nullptr && hipMemcpyFromSymbol(host, HIP_SYMBOL(w4::g_stamps), n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return COMET_ELAUNCH;
+  if (clear) {
+    static unsigned long long* zero = nullptr;
+    if (zero == nullptr) zero = (unsigned long long*)calloc(cap, 8);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(w4::g_stamps), zero, cap * 8, 0, hipMemcpyHostToDevice) != hipSuccess) return COMET_ELAUNCH;
+  }
+  return (int)n;
+}
+#endif
 
 extern "C" int comet_gemm(const comet_gemm_args* args, void* stream) {
   using namespace comet;

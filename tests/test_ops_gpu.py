@@ -927,3 +927,34 @@ def test_gemm_persistent_preact_bf16(mnk, act):
     _close(out, ref, 1e-2, 1e-2, f"pp preact {mnk} act{act}")
 
 
+
+
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("mnk", [(16, 768, 768), (16, 768, 2304), (128, 2304, 768), (128, 768, 3072), (48, 96, 640)])
+@pytest.mark.parametrize("out", [torch.float32, torch.bfloat16])
+def test_gemm_small_split_matches_unsplit(la, lb, mnk, out, monkeypatch):
+    """Few-tile short-K bf16 GEMMs (the camera trunk's M = 16-128 token GEMMs) split K over
+    workgroups (choose_splits); the split result equals the unsplit one to f32 summation order and
+    both are within bf16-operand tolerance of f64."""
+    ops = _ops()
+    M, N, K = mnk
+    A = _rand(M, K, dtype=torch.bfloat16, seed=21)
+    B = _rand(N, K, dtype=torch.bfloat16, seed=22)
+    bias = _rand(N, seed=23).to(DEV)
+    ref = A.double() @ B.double().t() + bias.double().cpu()
+    Ad = (A if la == 0 else A.t().contiguous()).to(DEV)
+    Bd = (B if lb == 0 else B.t().contiguous()).to(DEV)
+    res = {}
+    for mode in ("split", "nosplit"):
+        if mode == "nosplit":
+            monkeypatch.setenv("COMET_GEMM_NO_SMALLSPLIT", "1")
+        C = torch.full((M, N), float("nan"), device=DEV, dtype=out)
+        ops.gemm_raw(Ad, Bd, C, m=M, n=N, k=K, layout_a=la, lda=(K if la == 0 else M),
+                     layout_b=lb, ldb=(K if lb == 0 else N), ldc=N, bias=bias, bias_mode=1)
+        res[mode] = C.double().cpu()
+    monkeypatch.delenv("COMET_GEMM_NO_SMALLSPLIT", raising=False)
+    q = 2.0 ** -8 if out == torch.bfloat16 else 0.0
+    for mode, C in res.items():
+        _close(C, ref, q + 1e-5, 1e-4 * math.sqrt(K), f"{mode} {mnk} la={la} lb={lb} {out}")
+    d = (res["split"] - res["nosplit"]).abs().max().item()
+    assert d <= (2 * q + 1e-5) * ref.abs().max().item(), f"split vs unsplit differ by {d:.3e}"

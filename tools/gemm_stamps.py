@@ -1,0 +1,83 @@
+"""Per-tile phase timing of the persistent GEMM from the diagnostic build's clock stamps.
+
+    COMET_HIP_LIB=comet-pose-estimation_amd/libcomet_hip_stamp.so \
+        python tools/gemm_stamps.py M N K [act] [f32|bf16] [resid]
+
+(make -C comet-pose-estimation_amd STAMPS=1 builds the library.) Wave 0 of each workgroup stamps
+the shader clock at each tile's k-loop start (0), before (1) and after (2) its epilogue, and at the
+end after draining its stores (3). Prints, over the workgroups, the k-loop cycles per tile, the
+epilogue cycles per tile, the gap from one tile's epilogue end to the next tile's k-loop start, the
+first k-loop start (from the earliest workgroup start) and the store drain at the end.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "comet-pose-estimation_amd"))
+from comet_amd import _lib as L, ops  # noqa: E402
+
+WG, TILES = 256, 64
+
+
+def main():
+    M, N, K = (int(v) for v in sys.argv[1:4])
+    act = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    odt = torch.float32 if len(sys.argv) > 5 and sys.argv[5] == "f32" else torch.bfloat16
+    res = len(sys.argv) > 6 and sys.argv[6] == "1"
+    lib = L.load()
+    if not hasattr(lib, "comet_gemm_stamps"):
+        raise SystemExit(f"{L.LIB_PATH} is not the STAMPS=1 build")
+    lib.comet_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+    w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+    b = torch.rand(N, device="cuda")
+    r = torch.rand(M, N, device="cuda", dtype=odt) if res else None
+    out = torch.empty(M, N, device="cuda", dtype=odt)
+    for _ in range(20):  # warm (clock settles under load)
+        ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt)
+    torch.cuda.synchronize()
+    lib.comet_gemm_stamps(None, 0, 1)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3
+    buf = np.zeros(WG * TILES * 4, dtype=np.uint64)
+    lib.comet_gemm_stamps(buf.ctypes.data, buf.size, 0)
+    st = buf.reshape(WG, TILES, 4).astype(np.int64)
+    used = st[:, 0, 0] != 0
+    st = st[used]
+    t0 = st[:, 0, 0].min()
+    kl, ep, gap, ends = [], [], [], []
+    ntile = []
+    for w_ in st:
+        n = int(np.count_nonzero(w_[:, 0]))
+        ntile.append(n)
+        for t in range(n):
+            kl.append(w_[t, 1] - w_[t, 0])
+            ep.append(w_[t, 2] - w_[t, 1])
+            if t + 1 < n:
+                gap.append(w_[t + 1, 0] - w_[t, 2])
+        ends.append(w_[n, 3] - w_[n - 1, 2] if n < TILES and w_[n, 3] else 0)
+    span = max(w_[int(np.count_nonzero(w_[:, 0])) - 1, 2] for w_ in st) - t0
+    f = lambda a: f"mean {np.mean(a):8.0f}  p10 {np.percentile(a, 10):8.0f}  p90 {np.percentile(a, 90):8.0f}"  # noqa: E731
+    nk = K // 64
+    print(f"M{M} N{N} K{K} act{act} {odt} res{int(res)}: {us:.1f} us, {2 * M * N * K / us / 1e6:.0f} TF/s; "
+          f"{len(st)} workgroups, tiles per workgroup {min(ntile)}-{max(ntile)}, {nk} k-tiles per tile")
+    print(f"  k-loop per tile   (cycles) {f(kl)}   per k-tile {np.mean(kl) / nk:.0f}")
+    print(f"  epilogue per tile (cycles) {f(ep)}")
+    print(f"  gap to next tile  (cycles) {f(gap) if gap else '-'}")
+    print(f"  store drain at end (cycles) {f(ends)}")
+    print(f"  first k-loop start spread {np.percentile(st[:, 0, 0] - t0, 90):.0f} cycles (p90); "
+          f"span of stamps {span} cycles -> clock {span / us / 1e3:.2f} GHz if the span ~ kernel time")
+    print(f"  share: k-loop {np.sum(kl) / (np.sum(kl) + np.sum(ep) + np.sum(gap)):.3f}  "
+          f"epilogue {np.sum(ep) / (np.sum(kl) + np.sum(ep) + np.sum(gap)):.3f}")
+
+
+if __name__ == "__main__":
+    main()
