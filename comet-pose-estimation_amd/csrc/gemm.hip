@@ -42,6 +42,7 @@ struct Epi {
   int vec;  // output / resid / aux rows allow 8-wide vector access (host-checked)
   int wide = 0;  // persistent kernel: 16-B bf16 stores (C 16-B aligned, ldc % 8 == 0; host-checked)
   int prio = 0;  // persistent kernel: s_setprio 1 for waves 4-7 (COMET_GEMM_PRIO=1, measurement)
+  int bpark = 0;  // persistent kernel: bf16-park epilogue (COMET_GEMM_NO_BPARK=1: the direct / f32-park paths)
 };
 
 // Split-K partials: ws[((z * nb) + bz) * M * N + row * N + col], f32.
@@ -1034,22 +1035,33 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   // tile is 64 wide (tools/gpu/kscan.sh: the direct 4-column stores of 16 rows per instruction
   // cost ~3-4 us per 256 x 256 tile, 10-18 % of a K = 384-768 GEMM). With GELU the parked path
   // serialises the activation behind the LDS round trips (+27 %): those keep the direct stores.
-  constexpr bool PARK = std::is_same<TC, float>::value || (WCOLS % 64 == 0 && ACT == COMET_ACT_NONE);
+  constexpr bool BPARK = std::is_same<TC, __bf16>::value && !HASR && !LN && WCOLS == 64 && ACT == COMET_ACT_NONE;  // see below
+  constexpr bool PARK = std::is_same<TC, float>::value || (WCOLS % 64 == 0 && ACT == COMET_ACT_NONE && !BPARK);
   // direct bf16 stores of interior tiles without a residual: fragments j, j+1 exchange halves by
   // v_permlane16_swap so every lane stores 16 B (8 columns) instead of 8 B -- half the store
   // instructions for the same bytes (the epilogue tail is store-issue bound: cdna_hip_programming.md
   // T21). COMET_GEMM_NO_WIDE=1 at launch selects the 8-B stores (measurement A/B).
-  constexpr bool WIDE = !PARK && !HASR && std::is_same<TC, __bf16>::value && (NI % 2 == 0);
+  constexpr bool WIDE = !PARK && !BPARK && !HASR && std::is_same<TC, __bf16>::value && (NI % 2 == 0);
   // parked f32 row pitch: 64-wide slabs XOR-swizzle their 16-B chunks (c ^ pswz(r): the 8 rows
   // one ds_write_b128 lane group writes hit 8 distinct chunks and the 4 (row, 4-chunk) quads of
   // each ds_read_b128 lane group of the re-read are disjoint); 96-wide slabs pad rows to 100
+  // bf16 outputs without a residual or activation on 64-wide wave tiles (interior tiles, epi.bpark):
+  // the epilogue value (alpha * acc + bias) is parked as bf16, one 16-row block at a time, in a
+  // per-wave slab (two alternate), re-read as 8 rows x 128 B per ds_read_b128 and stored as whole
+  // 128-B lines: half the LDS bytes and write instructions of the f32 park (epilogue 8.9k -> 5.4k
+  // cycles per 256 x 256 tile, tools/gemm_stamps.py). GELU outputs keep the direct 16-B stores: their
+  // epilogue is VALU-bound on the activation and the park round trip measured 4 % slower.
+  constexpr int BSLAB = 16 * WCOLS;                   // bf16 elements of one slab
+  constexpr int BPARK_B = BPARK ? NW * 2 * BSLAB : 0;  // bf16 elements of the bf16 park region
   constexpr bool PSWZ = (WCOLS & (WCOLS - 1)) == 0;
   constexpr int PPITCH = PSWZ ? WCOLS : WCOLS + 4;
   constexpr int PARK_F = PARK ? NW * 8 * PPITCH : 0;  // f32 elements of the park region
   auto pswz = [](int r) { return PSWZ ? ((r & 7) | ((r & 2) << 2)) : 0; };
   static_assert(!LN || (PARK && std::is_same<TC, float>::value), "row LN epilogue: parked f32 outputs only");
+  static_assert(!LN || !BPARK, "row LN epilogue: no bf16 park");
   constexpr int STATS_F = LN ? 2 * TBM * WN : 0;  // f32 row-partial table (sum, sum of squares)
-  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + 2 * PARK_F + 2 * STATS_F];
+  constexpr int PARK_ELEMS = 2 * PARK_F > BPARK_B ? 2 * PARK_F : BPARK_B;
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + PARK_ELEMS + 2 * STATS_F];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / WN, wc = wid % WN;
@@ -1162,7 +1174,13 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // every wave's reads of buffer q&1 and LDS-DMA of k-tile q+1 are done past this barrier; after
     // an interior tile's epilogue its stores (all issued after that LDS-DMA) stay in flight
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (pend) {
+    if (pend == 2) {  // bf16-park epilogue: 2 x MI stores
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * MI) : "memory");
+      pend = 0;
+    } else if (pend == 3) {  // bf16-park epilogue with the pre-activation copy: 4 x MI stores
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * MI > 63 ? 63 : 4 * MI) : "memory");
+      pend = 0;
+    } else if (pend) {
       // VMEM ops per output kind of one epilogue: direct MI x NI, parked 2 x MI x (WCOLS / (8 * CPL))
       constexpr int PER = PARK ? 2 * MI * (WCOLS / (8 * (16 / (int)sizeof(TC)))) : (WIDE ? MI * NI / 2 : MI * NI);
       constexpr int E = PER * (1 + (HASR ? 1 : 0)) + PER;  // C stores (+ resid loads) (+ aux stores)
@@ -1183,6 +1201,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#ifdef COMET_GEMM_STAMPS
+    if (q % nk == (nk > 1 ? 1 : 0)) COMET_STAMP(q / nk, 3);
+#endif
     // ---- k-step 1: MFMAs on (a1, b1); LDS-DMA of k-tile q+2 into buffer q&1 (past the end of the
     // stream: a re-load of the last k-tile that nothing reads); reads of k-tile q+1's k-step-0
     // fragments (a0, b0) from buffer (q+1)&1 (garbage past the end, never used). Branch-free.
@@ -1204,7 +1225,6 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     }
     __builtin_amdgcn_sched_barrier(0);
     advance();
-
     if (!tile_end) continue;
     COMET_STAMP(q / nk, 1);
     // ---- epilogue of tile q / nk, straight from the accumulators: lane (li, g) of fragment
@@ -1324,8 +1344,10 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 #pragma unroll
           for (int t = 0; t < NTC; ++t) load4(epi.bias + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(bcp + t * CPL));
         }
-        // residual rows are loaded one (i, h) step ahead, so each step's HBM latency overlaps the
-        // previous step's park / reduce / store work instead of being exposed MI x 2 times
+        // residual rows are loaded one (i, h) step ahead (a 2-slot register ring), so each step's HBM
+        // latency overlaps the previous step's park / reduce / store work instead of being exposed
+        // MI x 2 times (a 3-slot ring measured 4 % slower on the 64 x 384 tiles)
+        constexpr int RDL = 2;
         auto rload = [&](int ih, float (&dst)[NTC][CPL]) {
           const int64_t row = prow0 + (ih >> 1) * 16 + (ih & 1) * 8;
 #pragma unroll
@@ -1338,8 +1360,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
               if (!EDGE || row < M) loadn<CPL>(R + row * epi.ldr + pc0 + t * 8 * CPL, dst[t]);
           }
         };
-        float rcur[NTC][CPL];
-        rload(0, rcur);
+        float rring[RDL][NTC][CPL];
+#pragma unroll
+        for (int d = 0; d < RDL - 1; ++d) rload(d, rring[d]);
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           float vh[2][NV];
@@ -1347,12 +1370,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
           for (int h = 0; h < 2; ++h) {
             const int64_t row = prow0 + i * 16 + h * 8;
             const bool live = !EDGE || row < M;
-            float rc[NTC][CPL], rnext[NTC][CPL];
-#pragma unroll
-            for (int t = 0; t < NTC; ++t)
-#pragma unroll
-              for (int e = 0; e < CPL; ++e) rc[t][e] = rcur[t][e];
-            if (2 * i + h + 1 < 2 * MI) rload(2 * i + h + 1, rnext);
+            const int ih = 2 * i + h;
+            float (&rc)[NTC][CPL] = rring[ih % RDL];
+            if (ih + RDL - 1 < 2 * MI) rload(ih + RDL - 1, rring[(ih + RDL - 1) % RDL]);
             if ((li >> 3) == h) {
 #pragma unroll
               for (int j = 0; j < NI; ++j)
@@ -1381,12 +1401,6 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
             sq = red8(sq);
             if (cc == 0) *reinterpret_cast<float2*>(st + 2 * (lrow(i, h) + wc)) = float2{s, sq};
             asm volatile("" ::: "memory");
-            if (2 * i + h + 1 < 2 * MI) {
-#pragma unroll
-              for (int t = 0; t < NTC; ++t)
-#pragma unroll
-                for (int e = 0; e < CPL; ++e) rcur[t][e] = rnext[t][e];
-            }
           }
 #pragma unroll
           for (int h = 0; h < 2; ++h)
@@ -1441,6 +1455,77 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       // the next tile's k-step-0 fragments again (buffer (q+1)&1 still holds k-tile q+1): the
       // copies read during k-step 1 are dead here, so their registers serve the epilogue
       read_frags((q + 1) & 1, 0, a0, b0);
+    } else if (BPARK && interior && epi.bpark) {
+      if constexpr (BPARK) {
+        __bf16* slab0 = smem + 2 * BUF + wid * 2 * BSLAB;
+        const int rr = lane >> 3, cc = lane & 7;
+        float bc[NI][4];
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bc[j][e] = 0.f;
+        if (epi.bias != nullptr) {  // one uniform branch around straight-line loads
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bc[j][e] = epi.bias[col0 + j * 16 + e];
+        }
+        // per-lane output bases: rows srow0 + i*16 + h*8 (the block offsets are uniform)
+        const int64_t srow0 = (int64_t)tm * TBM + wr * WROWS + rr;
+        const int64_t scol = (int64_t)tn * TBN + wc * WCOLS + cc * 8;
+        TC* cbase = C + srow0 * ldc + scol;
+        // slab layout: row r (0..15) of the block, 16-B chunk k stored at chunk k ^ (r & 7), and the
+        // two 8-B halves of a chunk swapped for rows 8..15 (the fragment writes -- rows li and li + 8
+        // in one lane group -- then hit distinct banks; the row reads are conflict-free)
+        const int wofs = li * WCOLS + ((g & 1) ^ (li >> 3)) * 4;
+        const int rofs = rr * WCOLS + ((cc ^ rr) << 3);
+        // PRE: the activation is applied before parking (no pre-activation copy); otherwise the parked
+        // pre-activation is stored to X and the activation applied to the re-read values. Two
+        // straight-line bodies: a per-element branch on X splits the GELU chains into basic blocks.
+        auto body = [&](auto pre_t) {
+          constexpr bool PRE = decltype(pre_t)::value;
+          TC* xbase = PRE ? nullptr : X + srow0 * epi.ldaux + scol;
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            __bf16* slab = slab0 + (i & 1) * BSLAB;
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+              float v[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v[e] = epi.alpha * acc[i][j][e] + bc[j][e];
+                if constexpr (PRE) v[e] = apply_act(ACT, v[e]);
+              }
+              *reinterpret_cast<uint2*>(slab + wofs + (((2 * j + (g >> 1)) ^ (li & 7)) << 3)) =
+                  uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+              acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              uint4 d = *reinterpret_cast<const uint4*>(slab + h * 8 * WCOLS + rofs);
+              if (h == 1) d = uint4{d.z, d.w, d.x, d.y};
+              const int64_t roff = (int64_t)(i * 16 + h * 8);
+              if constexpr (!PRE) {
+                *reinterpret_cast<uint4*>(xbase + roff * epi.ldaux) = d;
+                const unsigned u[4] = {d.x, d.y, d.z, d.w};
+                unsigned o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                  o[e] = pack_bf16x2(apply_act(ACT, bf16_lo(u[e])), apply_act(ACT, bf16_hi(u[e])));
+                d = uint4{o[0], o[1], o[2], o[3]};
+              }
+              *reinterpret_cast<uint4*>(cbase + roff * ldc) = d;
+            }
+            asm volatile("" ::: "memory");
+          }
+        };
+        if (X == nullptr) body(std::true_type{});
+        else body(std::false_type{});
+        read_frags((q + 1) & 1, 0, a0, b0);
+      }
+    } else if constexpr (BPARK) {
+      epilogue(std::true_type{});  // edge tiles (or unaligned outputs): masked direct stores
     } else if constexpr (PARK) {
       // parked epilogue: per 8-row half of each 16-row block the wave parks its 8 x WCOLS raw
       // accumulators in its own LDS slab (no barrier: only this wave touches it) and re-reads them
@@ -1468,21 +1553,31 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
               bcp[t][e] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
             }
         }
+        // residual rows prefetched RD (i, h) steps ahead into a register ring (the next tile's
+        // k-step-0 fragments are re-read after the epilogue, so their registers hold the ring):
+        // each step's residual load then has RD - 1 steps of park / store work to land in (3 steps:
+        // epilogue 39.5k -> 32.1k cycles per 256 x 256 f32 tile, K 3072 GEMM 835 -> 900 TF/s)
+        constexpr int NSTEP = 2 * MI, RD = HASR ? 4 : 1;
+        float rq[RD][NTC][CPL];
+        auto rld = [&](int st, float (&dst)[NTC][CPL]) {
+          const int64_t row = prow0 + (st >> 1) * 16 + (st & 1) * 8;
+#pragma unroll
+          for (int t = 0; t < NTC; ++t) {
+            const int64_t col = pcol0 + t * 8 * CPL;
+            if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, dst[t]);
+          }
+        };
+        if constexpr (HASR) {
+#pragma unroll
+          for (int d = 0; d < RD; ++d)
+            if (d < NSTEP) rld(d, rq[d]);
+        }
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            // residual of these 8 rows first (its wait covers the previous half's stores; a
-            // prefetch one block ahead spills at 256 VGPRs)
-            float rc[NTC][CPL];
+            float (&rc)[NTC][CPL] = rq[(2 * i + h) % RD];
             const int64_t row = prow0 + i * 16 + h * 8;
-            if constexpr (HASR) {
-#pragma unroll
-              for (int t = 0; t < NTC; ++t) {
-                const int64_t col = pcol0 + t * 8 * CPL;
-                if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, rc[t]);
-              }
-            }
             if ((li >> 3) == h) {
 #pragma unroll
               for (int j = 0; j < NI; ++j)
@@ -1512,6 +1607,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
                 storen<CPL>(C + row * ldc + col, v);
               }
             }
+            if constexpr (HASR) {
+              if (2 * i + h + RD < NSTEP) rld(2 * i + h + RD, rc);
+            }
             asm volatile("" ::: "memory");
             if (h == 1) {
 #pragma unroll
@@ -1521,6 +1619,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       };
       if (interior) pepilogue(std::false_type{});
       else pepilogue(std::true_type{});
+      if constexpr (HASR) read_frags((q + 1) & 1, 0, a0, b0);
     } else {
     if constexpr (WIDE) {
       if (interior && X == nullptr && epi.wide) {
@@ -1566,7 +1665,8 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     }
     // interior: every VMEM op this epilogue issued came after the LDS-DMA of k-tile q+2 and their
     // count is fixed, so the next barrier wait leaves them in flight
-    if constexpr (WIDE) pend = (interior && X == nullptr && epi.wide) ? 1 : 0;
+    if (BPARK && interior && epi.bpark) pend = X != nullptr ? 3 : 2;
+    else if constexpr (WIDE) pend = (interior && X == nullptr && epi.wide) ? 1 : 0;
     else pend = interior ? 1 : 0;
     COMET_STAMP(q / nk, 2);
   }
@@ -1678,6 +1778,8 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
   e.wide = (uintptr_t)a.c % 16 == 0 && a.ldc % 8 == 0 && getenv("COMET_GEMM_NO_WIDE") == nullptr;
   e.prio = getenv("COMET_GEMM_PRIO") != nullptr;
+  e.bpark = (uintptr_t)a.c % 16 == 0 && a.ldc % 8 == 0 && (a.aux == nullptr || ((uintptr_t)a.aux % 16 == 0 && a.ldaux % 8 == 0)) &&
+            getenv("COMET_GEMM_NO_BPARK") == nullptr;
   const w4::RowLN noln{};
   // N = 384 (the tracker's hidden size): 128 x 384 tiles (each A row block read once);
   // otherwise 256 x 256

@@ -25,7 +25,8 @@ WG, TILES = 256, 64
 
 def main():
     M, N, K = (int(v) for v in sys.argv[1:4])
-    act = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    ln_mode = sys.argv[4][3:] if len(sys.argv) > 4 and sys.argv[4].startswith("ln_") else None  # ln_norm2 / ln_dual / ln_dual_ctx
+    act = int(sys.argv[4]) if len(sys.argv) > 4 and ln_mode is None else 0
     odt = torch.float32 if len(sys.argv) > 5 and sys.argv[5] == "f32" else torch.bfloat16
     res = len(sys.argv) > 6 and sys.argv[6] == "1"
     lib = L.load()
@@ -37,13 +38,20 @@ def main():
     b = torch.rand(N, device="cuda")
     r = torch.rand(M, N, device="cuda", dtype=odt) if res else None
     out = torch.empty(M, N, device="cuda", dtype=odt)
+    if ln_mode is not None:  # row-LN GEMM (comet_gemm_rowln): f32 residual stream + LayerNorm epilogue
+        r = torch.rand(M, N, device="cuda")
+        z = (torch.rand(N, device="cuda"), torch.rand(N, device="cuda"), 1e-5) if ln_mode == "dual_ctx" else None
+        odt = torch.float32
+        call = lambda: ops.linear_rowln(x, w, b, r, raw=ln_mode == "norm2", y16_eps=1e-6, z=z)  # noqa: E731
+    else:
+        call = lambda: ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt)  # noqa: E731
     for _ in range(20):  # warm (clock settles under load)
-        ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt)
+        call()
     torch.cuda.synchronize()
     lib.comet_gemm_stamps(None, 0, 1)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    ops.linear(x, w, bias=b, act=act, resid=r, out=out, out_dtype=odt)
+    call()
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3
@@ -52,29 +60,27 @@ def main():
     st = buf.reshape(WG, TILES, 4).astype(np.int64)
     used = st[:, 0, 0] != 0
     st = st[used]
-    t0 = st[:, 0, 0].min()
-    kl, ep, gap, ends = [], [], [], []
+    kl, ep, gap, ends, kf = [], [], [], [], []
     ntile = []
     for w_ in st:
         n = int(np.count_nonzero(w_[:, 0]))
         ntile.append(n)
         for t in range(n):
             kl.append(w_[t, 1] - w_[t, 0])
+            kf.append(w_[t, 3] - w_[t, 0])
             ep.append(w_[t, 2] - w_[t, 1])
             if t + 1 < n:
                 gap.append(w_[t + 1, 0] - w_[t, 2])
-        ends.append(w_[n, 3] - w_[n - 1, 2] if n < TILES and w_[n, 3] else 0)
-    span = max(w_[int(np.count_nonzero(w_[:, 0])) - 1, 2] for w_ in st) - t0
+        ends.append(w_[n, 3] - w_[n - 1, 2] if n < TILES and w_[n, 3] else 0)  # tile n: only the end stamp
     f = lambda a: f"mean {np.mean(a):8.0f}  p10 {np.percentile(a, 10):8.0f}  p90 {np.percentile(a, 90):8.0f}"  # noqa: E731
-    nk = K // 64
-    print(f"M{M} N{N} K{K} act{act} {odt} res{int(res)}: {us:.1f} us, {2 * M * N * K / us / 1e6:.0f} TF/s; "
+    nk = K // 64  # (s_memtime counters are per XCD: only differences within a workgroup are used)
+    print(f"M{M} N{N} K{K} {('rowln ' + ln_mode) if ln_mode else f'act{act}'} {odt} res{int(res)}: {us:.1f} us, {2 * M * N * K / us / 1e6:.0f} TF/s; "
           f"{len(st)} workgroups, tiles per workgroup {min(ntile)}-{max(ntile)}, {nk} k-tiles per tile")
     print(f"  k-loop per tile   (cycles) {f(kl)}   per k-tile {np.mean(kl) / nk:.0f}")
+    print(f"  k-loop to the 2nd k-tile's barrier (cycles) {f(kf)}; rest per k-tile {(np.mean(kl) - np.mean(kf)) / max(nk - 1, 1):.0f}")
     print(f"  epilogue per tile (cycles) {f(ep)}")
     print(f"  gap to next tile  (cycles) {f(gap) if gap else '-'}")
     print(f"  store drain at end (cycles) {f(ends)}")
-    print(f"  first k-loop start spread {np.percentile(st[:, 0, 0] - t0, 90):.0f} cycles (p90); "
-          f"span of stamps {span} cycles -> clock {span / us / 1e3:.2f} GHz if the span ~ kernel time")
     print(f"  share: k-loop {np.sum(kl) / (np.sum(kl) + np.sum(ep) + np.sum(gap)):.3f}  "
           f"epilogue {np.sum(ep) / (np.sum(kl) + np.sum(ep) + np.sum(gap)):.3f}")
 

@@ -21,6 +21,6 @@ for line in out.splitlines():
         rows[cur][m.group(1).strip()] = int(m.group(2))
 for k, v in rows.items():
     if flt in k:
-        dem = subprocess.run(["c++filt", k], capture_output=True, text=True).stdout.strip()
+        dem = k if "--mangled" in sys.argv else subprocess.run(["c++filt", k], capture_output=True, text=True).stdout.strip()
         print(f"vgpr {v.get('VGPRs', '?'):>4} agpr {v.get('AGPRs', '?'):>3} scratch {v.get('ScratchSize', '?'):>4} "
               f"occ {v.get('Occupancy', '?')} lds {v.get('LDS Size', '?'):>6}  {dem[:150]}")
