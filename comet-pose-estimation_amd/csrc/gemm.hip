@@ -988,14 +988,15 @@ constexpr int SG_MFMA = 0x008, SG_DSR = 0x100, SG_VMR = 0x020;
 
 #ifdef COMET_GEMM_STAMPS
 // Diagnostic build only (make STAMPS=1 -> libcomet_hip_stamp.so): wave 0 of each workgroup records
-// the shader clock at the start of each tile's k-loop, before and after its epilogue; written by
+// the shader clock at the start of each tile's k-loop (0), before (1) and after (2) its epilogue,
+// past the second k-tile's barrier (3), and around the row-LN statistics barrier (4, 5); written by
 // lane 0 with a vector store into g_stamps[workgroup][tile][phase] (tools/gemm_stamps.py).
 constexpr int ST_WG = 256, ST_TILES = 64;
-__device__ unsigned long long g_stamps[ST_WG * ST_TILES * 4];
+__device__ unsigned long long g_stamps[ST_WG * ST_TILES * 8];
 __device__ __forceinline__ void stamp(int bid, int wid, int tile, int ph) {
   const unsigned long long t = __builtin_amdgcn_s_memtime();
   if (wid == 0 && bid < ST_WG && tile < ST_TILES && (threadIdx.x & 63) == 0)
-    g_stamps[((bid * ST_TILES + tile) << 2) + ph + (threadIdx.x & 63)] = t;
+    g_stamps[((bid * ST_TILES + tile) << 3) + ph + (threadIdx.x & 63)] = t;
 }
 #define COMET_STAMP(tile, ph) stamp(bid, wid, (tile), (ph))
 #else
@@ -1416,7 +1417,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
             load4(ln.zb + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(zb + t * CPL));
           }
         }
+        COMET_STAMP(q / nk, 4);
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        COMET_STAMP(q / nk, 5);
         // pass 2: outputs, row by row (mean / rstd once per row, affine weights loaded before the
         // barrier: a load issued after this epilogue's stores would wait for them)
 #pragma unroll
@@ -2531,7 +2534,7 @@ extern "C" int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_a
 // diagnostic build: copy out / clear the per-tile clock stamps of the persistent GEMM
 extern "C" int comet_gemm_stamps(unsigned long long* host, int64_t n, int clear) {
   using namespace comet;
-  const int64_t cap = (int64_t)w4::ST_WG * w4::ST_TILES * 4;
+  const int64_t cap = (int64_t)w4::ST_WG * w4::ST_TILES * 8;
   if (n > cap) n = cap;
   if (host != nullptr && hipMemcpyFromSymbol(host, HIP_SYMBOL(w4::g_stamps), n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return COMET_ELAUNCH;
   if (clear) {

@@ -55,12 +55,12 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3
-    buf = np.zeros(WG * TILES * 4, dtype=np.uint64)
+    buf = np.zeros(WG * TILES * 8, dtype=np.uint64)
     lib.comet_gemm_stamps(buf.ctypes.data, buf.size, 0)
-    st = buf.reshape(WG, TILES, 4).astype(np.int64)
+    st = buf.reshape(WG, TILES, 8).astype(np.int64)
     used = st[:, 0, 0] != 0
     st = st[used]
-    kl, ep, gap, ends, kf = [], [], [], [], []
+    kl, ep, gap, ends, kf, p1, bw = [], [], [], [], [], [], []
     ntile = []
     for w_ in st:
         n = int(np.count_nonzero(w_[:, 0]))
@@ -69,6 +69,9 @@ def main():
             kl.append(w_[t, 1] - w_[t, 0])
             kf.append(w_[t, 3] - w_[t, 0])
             ep.append(w_[t, 2] - w_[t, 1])
+            if w_[t, 4]:  # row-LN epilogue: pass 1 end (4), statistics barrier passed (5)
+                p1.append(w_[t, 4] - w_[t, 1])
+                bw.append(w_[t, 5] - w_[t, 4])
             if t + 1 < n:
                 gap.append(w_[t + 1, 0] - w_[t, 2])
         ends.append(w_[n, 3] - w_[n - 1, 2] if n < TILES and w_[n, 3] else 0)  # tile n: only the end stamp
@@ -79,6 +82,8 @@ def main():
     print(f"  k-loop per tile   (cycles) {f(kl)}   per k-tile {np.mean(kl) / nk:.0f}")
     print(f"  k-loop to the 2nd k-tile's barrier (cycles) {f(kf)}; rest per k-tile {(np.mean(kl) - np.mean(kf)) / max(nk - 1, 1):.0f}")
     print(f"  epilogue per tile (cycles) {f(ep)}")
+    if p1:
+        print(f"  row-LN pass 1 {f(p1)}; statistics barrier {f(bw)}")
     print(f"  gap to next tile  (cycles) {f(gap) if gap else '-'}")
     print(f"  store drain at end (cycles) {f(ends)}")
     print(f"  share: k-loop {np.sum(kl) / (np.sum(kl) + np.sum(ep) + np.sum(gap)):.3f}  "
