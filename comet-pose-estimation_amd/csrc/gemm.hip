@@ -1174,6 +1174,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     __builtin_amdgcn_sched_group_barrier(SG_MFMA, NMF % NRD, 0);
     // every wave's reads of buffer q&1 and LDS-DMA of k-tile q+1 are done past this barrier; after
     // an interior tile's epilogue its stores (all issued after that LDS-DMA) stay in flight
+#ifdef COMET_GEMM_STAMPS
+    if (nk > 1 && q % nk == 1) COMET_STAMP(q / nk, 7);  // k-tile 1: before its wait + barrier
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (pend == 2) {  // bf16-park epilogue: 2 x MI stores
       asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * MI) : "memory");
@@ -1204,6 +1207,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     __builtin_amdgcn_sched_barrier(0);
 #ifdef COMET_GEMM_STAMPS
     if (q % nk == (nk > 1 ? 1 : 0)) COMET_STAMP(q / nk, 3);
+    if (nk > 1 && q % nk == 0) COMET_STAMP(q / nk, 6);  // k-tile 0 past its barrier
 #endif
     // ---- k-step 1: MFMAs on (a1, b1); LDS-DMA of k-tile q+2 into buffer q&1 (past the end of the
     // stream: a re-load of the last k-tile that nothing reads); reads of k-tile q+1's k-step-0

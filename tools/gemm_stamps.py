@@ -60,7 +60,7 @@ def main():
     st = buf.reshape(WG, TILES, 8).astype(np.int64)
     used = st[:, 0, 0] != 0
     st = st[used]
-    kl, ep, gap, ends, kf, p1, bw = [], [], [], [], [], [], []
+    kl, ep, gap, ends, kf, p1, bw, k0, k1s, k1w = [], [], [], [], [], [], [], [], [], []
     ntile = []
     for w_ in st:
         n = int(np.count_nonzero(w_[:, 0]))
@@ -68,6 +68,10 @@ def main():
         for t in range(n):
             kl.append(w_[t, 1] - w_[t, 0])
             kf.append(w_[t, 3] - w_[t, 0])
+            if w_[t, 6] and w_[t, 7]:  # k-tile 0 past its barrier (6); k-tile 1 before its wait (7)
+                k0.append(w_[t, 6] - w_[t, 0])
+                k1s.append(w_[t, 7] - w_[t, 6])
+                k1w.append(w_[t, 3] - w_[t, 7])
             ep.append(w_[t, 2] - w_[t, 1])
             if w_[t, 4]:  # row-LN epilogue: pass 1 end (4), statistics barrier passed (5)
                 p1.append(w_[t, 4] - w_[t, 1])
@@ -81,6 +85,9 @@ def main():
           f"{len(st)} workgroups, tiles per workgroup {min(ntile)}-{max(ntile)}, {nk} k-tiles per tile")
     print(f"  k-loop per tile   (cycles) {f(kl)}   per k-tile {np.mean(kl) / nk:.0f}")
     print(f"  k-loop to the 2nd k-tile's barrier (cycles) {f(kf)}; rest per k-tile {(np.mean(kl) - np.mean(kf)) / max(nk - 1, 1):.0f}")
+    if k0:
+        print(f"  k-tile 0 to its barrier passed {f(k0)}; k-step 1 + k-tile 1's k-step 0 {f(k1s)}; "
+              f"k-tile 1's wait + barrier {f(k1w)}")
     print(f"  epilogue per tile (cycles) {f(ep)}")
     if p1:
         print(f"  row-LN pass 1 {f(p1)}; statistics barrier {f(bw)}")
