@@ -174,6 +174,28 @@ def test_gemm_epilogue_bias_gelu_resid_aux(dtype):
     _close(aux, pre, tol, 1e-3, "epilogue aux")
 
 
+@pytest.mark.parametrize("mnk", [(257, 384, 64), (4096, 1536, 384)])
+def test_gemm_gelu_epilogue_precision(mnk):
+    """The epilogue GELU (csrc/common.hpp gelu_erf, exp2-polynomial form; tools/gelu_fit.py) against the f64
+    erf GELU of the kernel's own f32 pre-activation (aux): pre-activations over [-12, 12] via the bias,
+    |err| <= 3e-7 + one f32 rounding of the output (the fit's bound is 2.8e-7)."""
+    ops = _ops()
+    M, N, K = mnk
+    x = _rand(M, K, dtype=torch.bfloat16, seed=7)
+    w = _rand(N, K, dtype=torch.bfloat16, seed=8, scale=0.02)
+    b = torch.linspace(-12, 12, N)
+    out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    aux = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=1, out=out, aux=aux)
+    pre = aux.double()
+    assert pre.min().item() < -11 and pre.max().item() > 11
+    ref = F.gelu(pre)
+    err = (out.double() - ref).abs()
+    bound = 3e-7 + 2 ** -24 * ref.abs()
+    assert (err <= bound).all(), f"GELU epilogue: max err {err.max().item():.3e} at pre {pre.flatten()[err.argmax()].item():.4f}"
+    assert torch.isfinite(out).all()
+
+
 def test_gemm_batched_strided():
     ops = _ops()
     # per (b, h): C = Q_bh K_bh^T with q/k packed [B, L, 3, H, D]
