@@ -233,6 +233,9 @@ def test_ddp_simulated_ranks_equal_B2_gradients(size):
     torch.cuda.synchronize()
     ref = {k: p.grad for k, p in model.camera_predictor.named_parameters() if p.grad is not None}
     norm_tol, elem_tol = (1e-4, 1e-4) if dtype == torch.float32 else (2e-2, 3e-2)
+    # absolute floor for tiny-norm gradients (confidence_attention.2.weight: norm 8.4e-4, the B = 1 vs
+    # B = 2 summation orders differ by 2.2e-7 after the round-3 GELU change moved its inputs by an ulp)
+    floor = 1e-6
     worst = 0.0
     for rank in (0, 1):
         res, g, during, nb, _ = got[rank]
@@ -242,7 +245,7 @@ def test_ddp_simulated_ranks_equal_B2_gradients(size):
             for k, n in res[step].items():
                 r = ref[k].double().norm().item()
                 worst = max(worst, abs(n - r) / max(r, 1e-12))
-                assert abs(n - r) <= norm_tol * r + 1e-7, (rank, step, k, n, r)
+                assert abs(n - r) <= norm_tol * r + floor, (rank, step, k, n, r)
         for k, v in g.items():
             e = (torch.from_numpy(v).double() - ref[k].cpu().double()).abs().max().item()
             rel = e / ref[k].abs().max().item()
