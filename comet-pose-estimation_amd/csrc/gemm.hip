@@ -1062,7 +1062,24 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   static_assert(!LN || !BPARK, "row LN epilogue: no bf16 park");
   constexpr int STATS_F = LN ? 2 * TBM * WN : 0;  // f32 row-partial table (sum, sum of squares)
   constexpr int PARK_ELEMS = 2 * PARK_F > BPARK_B ? 2 * PARK_F : BPARK_B;
-  __shared__ __attribute__((aligned(1024))) __bf16 smem[2 * BUF + PARK_ELEMS + 2 * STATS_F];
+  // A-operand lookahead (AR): the A images (activation rows, streamed from HBM once when tiles_n is
+  // small) run in a 3-slot ring one k-tile ahead of the 2-slot B ring (weights, L2-resident). Within
+  // an issue batch the B pieces go first, so the barrier wait can leave the batch's A pieces in
+  // flight (vmcnt counts in issue order): each A load gets two k-tiles of MFMA work to land in
+  // instead of one. Taken by every instance whose LDS still fits (the row tiles up to 128 x 384 /
+  // 128 x 256 without an f32 park of 128 x 384); COMET_GEMM_NO_AR at build time disables it (A/B).
+#ifdef COMET_GEMM_NO_AR
+  constexpr bool AR = false;
+#else
+  constexpr bool AR = 2 * (3 * ASTAGE + 2 * TBN * BK + PARK_ELEMS + 2 * STATS_F) <= 160 * 1024 && TBM <= 128;
+#endif
+  constexpr int NA = AR ? 3 : 2;                  // A ring slots
+  constexpr int BSTAGE = TBN * BK;                // bf16 elements of the B image of one k-tile
+  constexpr int BRING = NA * ASTAGE;              // B ring base (A ring first)
+  constexpr int RING = NA * ASTAGE + 2 * BSTAGE;  // both rings (= 2 * BUF without AR)
+  constexpr int XA = AR ? PA : 0;                 // A pieces a barrier wait may leave in flight
+  static_assert(AR || RING == 2 * BUF, "ring layout");
+  __shared__ __attribute__((aligned(1024))) __bf16 smem[RING + PARK_ELEMS + 2 * STATS_F];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid / WN, wc = wid % WN;
@@ -1082,52 +1099,88 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   const int prowa = wid * PA * 8 + (lane >> 3), prowb = wid * PB * 8 + (lane >> 3);  // + p * 8
   // load-stream state: the k-tile the next issue_cur() loads (tile ld_it of this workgroup, k-tile
   // ld_kt of it); per tile, uniform row-block bases and per-lane 32-bit element offsets
-  int ld_it = 0, ld_kt = 0;
+  // (two streams, A and B: with AR the A stream runs one k-tile ahead, otherwise in lockstep)
+  int la_it = 0, la_kt = 0, lb_it = 0, lb_kt = 0;
   const __bf16* ldA = A;
   const __bf16* ldB = B;
   int offA[PA], offB[PB];
-  auto set_load_tile = [&](int it) {
+  // chunk swizzle of image row r: c ^ ((r >> 1) & 7) (r = this lane's row in the image)
+  auto lch = [&](int r) { return ((lane & 7) ^ ((r >> 1) & 7)) * 8; };
+  auto set_tile_a = [&](int it) {
     int tm, tn;
     tile_rc(off + it * G, tiles_m, tiles_n, tm, tn);
-    const int m0 = tm * TBM, n0 = tn * TBN;
+    const int m0 = tm * TBM;
     ldA = A + (int64_t)m0 * lda;
-    ldB = B + (int64_t)n0 * ldb;
-    // chunk swizzle of image row r: c ^ ((r >> 1) & 7) (r = this lane's row in the image)
-    auto lch = [&](int r) { return ((lane & 7) ^ ((r >> 1) & 7)) * 8; };
 #pragma unroll
     for (int p = 0; p < PA; ++p)
       offA[p] = (min(m0 + prowa + p * 8, (int)M - 1) - m0) * (int)lda + lch(prowa + p * 8);
+  };
+  auto set_tile_b = [&](int it) {
+    int tm, tn;
+    tile_rc(off + it * G, tiles_m, tiles_n, tm, tn);
+    const int n0 = tn * TBN;
+    ldB = B + (int64_t)n0 * ldb;
 #pragma unroll
     for (int p = 0; p < PB; ++p)
       offB[p] = (min(n0 + prowb + p * 8, (int)N - 1) - n0) * (int)ldb + lch(prowb + p * 8);
   };
-  auto issue_cur = [&](int buf) {
-    const __bf16* pa = ldA + ld_kt * BK;
-    const __bf16* pb = ldB + ld_kt * BK;
+  auto issue_a = [&](int slot) {
+    const __bf16* pa = ldA + la_kt * BK;
 #pragma unroll
-    for (int p = 0; p < (PA > PB ? PA : PB); ++p) {
-      if (p < PA)
-        __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + buf * BUF + (wid * PA + p) * 512), 16, 0, 0);
-      if (p < PB)
-        __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]),
-                                         (lds_void*)(smem + buf * BUF + ASTAGE + (wid * PB + p) * 512), 16, 0, 0);
+    for (int p = 0; p < PA; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + slot * ASTAGE + (wid * PA + p) * 512), 16, 0, 0);
+  };
+  auto issue_b = [&](int slot) {
+    const __bf16* pb = ldB + lb_kt * BK;
+#pragma unroll
+    for (int p = 0; p < PB; ++p)
+      __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]),
+                                       (lds_void*)(smem + BRING + slot * BSTAGE + (wid * PB + p) * 512), 16, 0, 0);
+  };
+  // one batch: A and B pieces interleaved (lockstep), or all B pieces before the A pieces (AR)
+  auto issue_cur = [&](int aslot, int bslot) {
+    if constexpr (AR) {
+      issue_b(bslot);
+      issue_a(aslot);
+    } else {
+      const __bf16* pa = ldA + la_kt * BK;
+      const __bf16* pb = ldB + lb_kt * BK;
+#pragma unroll
+      for (int p = 0; p < (PA > PB ? PA : PB); ++p) {
+        if (p < PA)
+          __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + aslot * ASTAGE + (wid * PA + p) * 512), 16, 0, 0);
+        if (p < PB)
+          __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]),
+                                           (lds_void*)(smem + BRING + bslot * BSTAGE + (wid * PB + p) * 512), 16, 0, 0);
+      }
     }
   };
-  // past the last k-tile the stream keeps re-loading it (into a buffer nothing reads again)
-  auto advance = [&]() {
-    if (++ld_kt == nk) {
-      if (ld_it + 1 < my_tiles) { ld_kt = 0; set_load_tile(++ld_it); }
-      else ld_kt = nk - 1;
+  // past the last k-tile a stream keeps re-loading it (into a slot nothing reads again)
+  auto advance_a = [&]() {
+    if (++la_kt == nk) {
+      if (la_it + 1 < my_tiles) { la_kt = 0; set_tile_a(++la_it); }
+      else la_kt = nk - 1;
     }
+  };
+  auto advance_b = [&]() {
+    if (++lb_kt == nk) {
+      if (lb_it + 1 < my_tiles) { lb_kt = 0; set_tile_b(++lb_it); }
+      else lb_kt = nk - 1;
+    }
+  };
+  auto advance = [&]() {
+    advance_a();
+    advance_b();
   };
 
   bf16x8 a0[MI], b0[NI], a1[MI], b1[NI];
-  auto read_frags = [&](int buf, int s, bf16x8 (&af)[MI], bf16x8 (&bf)[NI]) {
-    const __bf16* img = smem + buf * BUF;
+  auto read_frags = [&](int aslot, int bslot, int s, bf16x8 (&af)[MI], bf16x8 (&bf)[NI]) {
+    const __bf16* aimg = smem + aslot * ASTAGE;
+    const __bf16* bimg = smem + BRING + bslot * BSTAGE;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) af[i] = big::frag(img, wr * WROWS + i * 16 + li, 4 * s + g);
+    for (int i = 0; i < MI; ++i) af[i] = big::frag(aimg, wr * WROWS + i * 16 + li, 4 * s + g);
 #pragma unroll
-    for (int j = 0; j < NI; ++j) bf[j] = big::frag(img + ASTAGE, wc * WCOLS + j * 16 + li, 4 * s + g);
+    for (int j = 0; j < NI; ++j) bf[j] = big::frag(bimg, wc * WCOLS + j * 16 + li, 4 * s + g);
   };
 
   f32x4 acc[MI][NI];
@@ -1147,23 +1200,40 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   if (epi.prio && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   int pend = 0;  // 1: the last epilogue's stores are the newest VMEM ops (count known)
   // ---- prologue: k-tiles 0 and 1 in flight, k-tile 0 landed, its first-k-step fragments read
-  set_load_tile(0);
-  issue_cur(0);
-  advance();
-  if (T > 1) {
-    issue_cur(1);
+  set_tile_a(0);
+  set_tile_b(0);
+  if constexpr (AR) {
+    // B0 A0 A1 | B1 A2: the wait leaves A1 and the second batch in flight (past the end of a short
+    // stream the extra pieces re-load the last k-tile into slots nothing reads)
+    issue_b(0);
+    advance_b();
+    issue_a(0);
+    advance_a();
+    issue_a(1);
+    advance_a();
+    issue_cur(2, 1);
     advance();
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PA + PB) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PA + PB) : "memory");
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    issue_cur(0, 0);
+    advance();
+    if (T > 1) {
+      issue_cur(1, 1);
+      advance();
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PA + PB) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   asm volatile("s_barrier" ::: "memory");
-  read_frags(0, 0, a0, b0);
+  read_frags(0, 0, 0, a0, b0);
+  int qa = 0;  // q % NA: the A slot of k-tile q (its B slot is q & 1)
 
   for (int q = 0; q < T; ++q) {
+    const int qa1 = qa + 1 == NA ? 0 : qa + 1;
     if (q % nk == 0) COMET_STAMP(q / nk, 0);
     // ---- k-step 0 of k-tile q: MFMAs on (a0, b0), reads of the k-step-1 fragments (a1, b1)
-    read_frags(q & 1, 1, a1, b1);
+    read_frags(qa, q & 1, 1, a1, b1);
     mfmas(a0, b0);
 #pragma unroll
     for (int t = 0; t < NRD; ++t) {
@@ -1179,10 +1249,10 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 #endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (pend == 2) {  // bf16-park epilogue: 2 x MI stores
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * MI) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA + 2 * MI > 63 ? 63 : XA + 2 * MI) : "memory");
       pend = 0;
     } else if (pend == 3) {  // bf16-park epilogue with the pre-activation copy: 4 x MI stores
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(4 * MI > 63 ? 63 : 4 * MI) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA + 4 * MI > 63 ? 63 : XA + 4 * MI) : "memory");
       pend = 0;
     } else if (pend) {
       // VMEM ops per output kind of one epilogue: direct MI x NI, parked 2 x MI x (WCOLS / (8 * CPL))
@@ -1193,14 +1263,14 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
         // (a lower bound of the VMEM ops issued after the LDS-DMA: bias / affine loads only add)
         constexpr int E1 = E - PER, E2 = E1 + PER, E3 = E1 + 2 * PER;
         const int nb = (ln.y16 != nullptr) + (ln.z16 != nullptr);
-        if (nb == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E1 > 63 ? 63 : E1) : "memory");
-        else if (nb == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E2 > 63 ? 63 : E2) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E3 > 63 ? 63 : E3) : "memory");
-      } else if (epi.aux) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E > 63 ? 63 : E) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(E - PER > 63 ? 63 : E - PER) : "memory");
+        if (nb == 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA + E1 > 63 ? 63 : XA + E1) : "memory");
+        else if (nb == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA + E2 > 63 ? 63 : XA + E2) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA + E3 > 63 ? 63 : XA + E3) : "memory");
+      } else if (epi.aux) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA + E > 63 ? 63 : XA + E) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA + E - PER > 63 ? 63 : XA + E - PER) : "memory");
       pend = 0;
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA) : "memory");
     }
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_barrier" ::: "memory");
@@ -1214,8 +1284,8 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // fragments (a0, b0) from buffer (q+1)&1 (garbage past the end, never used). Branch-free.
     const bool tile_end = (q + 1) % nk == 0;
     {
-      issue_cur(q & 1);
-      read_frags((q + 1) & 1, 0, a0, b0);
+      issue_cur(qa, q & 1);
+      read_frags(qa1, (q + 1) & 1, 0, a0, b0);
       mfmas(a1, b1);
       // per group of NMF / NRD MFMAs: one fragment read; LDS-DMA pieces (PA + PB) spread evenly
 #pragma unroll
@@ -1230,6 +1300,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     }
     __builtin_amdgcn_sched_barrier(0);
     advance();
+    qa = qa1;
     if (!tile_end) continue;
     COMET_STAMP(q / nk, 1);
     // ---- epilogue of tile q / nk, straight from the accumulators: lane (li, g) of fragment
@@ -1312,8 +1383,8 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       // the LDS table st (one barrier; var = E[v^2] - mean^2, clamped at 0). Pass 2 writes the
       // outputs with the statistics read back per row (no per-row arrays in registers).
       constexpr int CPL = 4, NTC = WCOLS / (8 * CPL), NV = NTC * CPL;
-      float* park = reinterpret_cast<float*>(smem + 2 * BUF) + wid * 8 * PPITCH;
-      float* st = reinterpret_cast<float*>(smem + 2 * BUF + 2 * PARK_F);
+      float* park = reinterpret_cast<float*>(smem + RING) + wid * 8 * PPITCH;
+      float* st = reinterpret_cast<float*>(smem + RING + 2 * PARK_F);
       const int rr = lane >> 3, cc = lane & 7;
       const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;  // + i*16 + h*8
       // (tn is always 0 here; keeping it in the column makes the bias / affine loads tile-dependent
@@ -1461,10 +1532,10 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       else lnepilogue(std::true_type{});
       // the next tile's k-step-0 fragments again (buffer (q+1)&1 still holds k-tile q+1): the
       // copies read during k-step 1 are dead here, so their registers serve the epilogue
-      read_frags((q + 1) & 1, 0, a0, b0);
+      read_frags(qa1, (q + 1) & 1, 0, a0, b0);
     } else if (BPARK && interior && epi.bpark) {
       if constexpr (BPARK) {
-        __bf16* slab0 = smem + 2 * BUF + wid * 2 * BSLAB;
+        __bf16* slab0 = smem + RING + wid * 2 * BSLAB;
         const int rr = lane >> 3, cc = lane & 7;
         float bc[NI][4];
 #pragma unroll
@@ -1529,7 +1600,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
         };
         if (X == nullptr) body(std::true_type{});
         else body(std::false_type{});
-        read_frags((q + 1) & 1, 0, a0, b0);
+        read_frags(qa1, (q + 1) & 1, 0, a0, b0);
       }
     } else if constexpr (BPARK) {
       epilogue(std::true_type{});  // edge tiles (or unaligned outputs): masked direct stores
@@ -1539,7 +1610,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       // row-contiguously, so every store / residual load instruction covers 8 rows x 128 B
       constexpr int CPL = 16 / (int)sizeof(TC);       // output columns per lane per access (16 B)
       constexpr int NTC = WCOLS / (8 * CPL);          // column passes per row
-      float* park = reinterpret_cast<float*>(smem + 2 * BUF) + wid * 8 * PPITCH;
+      float* park = reinterpret_cast<float*>(smem + RING) + wid * 8 * PPITCH;
       const int rr = lane >> 3, cc = lane & 7;
       const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;        // + i*16 + h*8
       const int64_t pcol0 = (int64_t)tn * TBN + wc * WCOLS + cc * CPL;  // + t*8*CPL
@@ -1626,7 +1697,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       };
       if (interior) pepilogue(std::false_type{});
       else pepilogue(std::true_type{});
-      if constexpr (HASR) read_frags((q + 1) & 1, 0, a0, b0);
+      if constexpr (HASR) read_frags(qa1, (q + 1) & 1, 0, a0, b0);
     } else {
     if constexpr (WIDE) {
       if (interior && X == nullptr && epi.wide) {

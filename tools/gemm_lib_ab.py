@@ -23,6 +23,12 @@ SHAPES = [  # (M, N, K, act, out dtype, resid, aux)
     (73856, 3072, 768, 1, torch.bfloat16, False, True),
     (74368, 768, 3072, 0, torch.float32, True, False),
     (8192, 8192, 8192, 0, torch.bfloat16, False, False),
+    # the virtual-track shapes (M = 8192: 128 x 384 / 64 x 384 / 128 x 256 tiles)
+    (8192, 1536, 384, 1, torch.bfloat16, False, False),
+    (8192, 1152, 384, 0, torch.bfloat16, False, False),
+    (8192, 768, 384, 0, torch.bfloat16, False, False),
+    (8192, 384, 384, 0, torch.bfloat16, False, False),
+    (8192, 384, 1536, 0, torch.float32, True, False),
 ]
 
 
