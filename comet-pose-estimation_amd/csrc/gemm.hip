@@ -159,8 +159,7 @@ __device__ __forceinline__ void write_tile_lds(const f32x4 (&acc)[MI][4], float*
     for (int e = 0; e < 8; ++e) v[e] = epi.alpha * v[e] + bc[e] + br;
     if (full) {
       if (X) store8(X + row * epi.ldaux + col0, v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = apply_act(epi.act, v[e]);
+      apply_act_n<8>(epi.act, v);
       if (R) {
         float r[8];
         load8(R + row * epi.ldr + col0, r);
@@ -645,7 +644,8 @@ gemm_skinny_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __re
       if (n0 >= N) continue;
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = apply_act(epi.act, epi.alpha * acc[nt][r] + bias4[nt][r]);
+      for (int r = 0; r < 4; ++r) v[r] = epi.alpha * acc[nt][r] + bias4[nt][r];
+      apply_act_n<4>(epi.act, v);
       if (R) {
         float rr[4];
         load4(R + m * epi.ldr + n0, rr);
@@ -927,8 +927,7 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
       for (int e = 0; e < 8; ++e) v[e] = epi.alpha * v[e] + bc[e] + br;
       if (epi.vec && col0 + 8 <= N) {
         if (X) store8(X + row * epi.ldaux + col0, v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = apply_act(epi.act, v[e]);
+        apply_act_n<8>(epi.act, v);
         if (R) {
           float rr[8];
           load8(R + row * epi.ldr + col0, rr);
@@ -1357,8 +1356,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = epi.alpha * acc[i][j][r] + bc[j][r];
             if (X) store4(X + row * epi.ldaux + col, v);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = apply_act(ACT, v[r]);
+            apply_act_n<4>(ACT, v);
             if constexpr (HASR) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] += epi.beta * rc[j][r];
@@ -1676,8 +1674,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 #pragma unroll
                 for (int e = 0; e < CPL; ++e) v[e] = epi.alpha * v[e] + bcp[t][e];
                 if (X) storen<CPL>(X + row * epi.ldaux + col, v);
-#pragma unroll
-                for (int e = 0; e < CPL; ++e) v[e] = apply_act(ACT, v[e]);
+                apply_act_n<CPL>(ACT, v);
                 if constexpr (HASR) {
 #pragma unroll
                   for (int e = 0; e < CPL; ++e) v[e] += epi.beta * rc[t][e];
@@ -1721,7 +1718,8 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
             for (int u = 0; u < 2; ++u) {
               float v[4];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = apply_act(ACT, epi.alpha * acc[i][j + u][e] + bc[j + u][e]);
+              for (int e = 0; e < 4; ++e) v[e] = epi.alpha * acc[i][j + u][e] + bc[j + u][e];
+              apply_act_n<4>(ACT, v);
               pk[u][0] = pack_bf16x2(v[0], v[1]);
               pk[u][1] = pack_bf16x2(v[2], v[3]);
               acc[i][j + u] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2284,7 +2282,8 @@ conv_skinny_kernel(const __bf16* __restrict__ X, int H, int W, int Cin, int KW, 
       if (n0 >= N) continue;
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = apply_act(epi.act, acc[nt][r] + bias4[nt][r]);
+      for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] + bias4[nt][r];
+      apply_act_n<4>(epi.act, v);
       if (R) {
         float rr[4];
         load4(R + m * epi.ldr + n0, rr);
