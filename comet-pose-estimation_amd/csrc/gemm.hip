@@ -2248,49 +2248,82 @@ conv_skinny_kernel(const __bf16* __restrict__ X, int H, int W, int Cin, int KW, 
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * 256) >> 6;
   const unsigned short* x16 = reinterpret_cast<const unsigned short*>(X);
-  for (int64_t m0 = wave * 16; m0 < M; m0 += nwaves * 16) {
-    const int64_t m = m0 + li;
+  // input fragments of the next 16-pixel step are gathered right after this step's MFMAs (software
+  // pipelined: the gather latency overlaps the epilogue); pixel -> (image, oy, ox) in 32-bit
+  // arithmetic (M < 2^31, host-checked: three 64-bit divisions per step cost more than its MFMAs)
+  auto gather = [&](int64_t m0, bf16x8 (&xf)[KC]) {
+    const int m = (int)m0 + li;
     const bool mok = m < M;
     int iy0 = 0, ix0 = 0;
     int64_t base = 0;
     if (mok) {
-      const int ox = (int)(m % OW);
-      const int64_t t = m / OW;
-      const int oy = (int)(t % OH);
-      const int64_t ni = t / OH;
+      const unsigned t = (unsigned)m / (unsigned)OW;
+      const int ox = m - (int)t * OW;
+      const unsigned ni = t / (unsigned)OH;
+      const int oy = (int)t - (int)ni * OH;
       iy0 = oy * stride - pad;
       ix0 = ox * stride - pad;
-      base = ni * H * W * Cin;
+      base = (int64_t)ni * H * W * Cin;
     }
-    f32x4 acc[NT16];
-#pragma unroll
-    for (int nt = 0; nt < NT16; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < KC; ++c) {
       const int k0 = 32 * c + 8 * g;
       const int iy = iy0 + tky[c], ix = ix0 + tkx[c];
       const bool ok = mok && k0 < K && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      const bf16x8 xf = ok ? *reinterpret_cast<const bf16x8*>(x16 + base + ((int64_t)iy * W + ix) * Cin + tci[c])
-                           : bf16x8{};
-#pragma unroll
-      for (int nt = 0; nt < NT16; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt][c], xf, acc[nt], 0, 0, 0);
+      xf[c] = ok ? *reinterpret_cast<const bf16x8*>(x16 + base + ((int64_t)iy * W + ix) * Cin + tci[c]) : bf16x8{};
     }
+  };
+  // 16-B bf16 stores (epi.wide, host-checked: cout % 32 == 0, Y 16-B aligned, ldy % 8 == 0): channel
+  // blocks nt, nt + 1 exchange lane-group halves by v_permlane16_swap so a lane stores 8 channels
+  constexpr bool WIDE = std::is_same<TC, __bf16>::value && NT16 % 2 == 0;
+  bf16x8 xa[KC], xb[KC];
+  gather(wave * 16, xa);
+  for (int64_t m0 = wave * 16; m0 < M; m0 += nwaves * 16) {
+    const int64_t m = m0 + li;
+    const bool mok = m < M;
+    f32x4 acc[NT16];
+#pragma unroll
+    for (int nt = 0; nt < NT16; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+      for (int nt = 0; nt < NT16; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt][c], xa[c], acc[nt], 0, 0, 0);
+    if (m0 + nwaves * 16 < M) gather(m0 + nwaves * 16, xb);
+#pragma unroll
+    for (int c = 0; c < KC; ++c) xa[c] = xb[c];
     if (!mok) continue;
+    float v[NT16][4];
 #pragma unroll
     for (int nt = 0; nt < NT16; ++nt) {
       const int n0 = nt * 16 + 4 * g;
-      if (n0 >= N) continue;
-      float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] + bias4[nt][r];
-      apply_act_n<4>(epi.act, v);
-      if (R) {
+      for (int r = 0; r < 4; ++r) v[nt][r] = acc[nt][r] + bias4[nt][r];
+      apply_act_n<4>(epi.act, v[nt]);
+      if (R && n0 < N) {
         float rr[4];
         load4(R + m * epi.ldr + n0, rr);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += epi.beta * rr[r];
+        for (int r = 0; r < 4; ++r) v[nt][r] += epi.beta * rr[r];
       }
-      store4(Y + m * ldy + n0, v);
+    }
+    if (WIDE && epi.wide) {
+      if constexpr (WIDE) {
+        const int wcol = 16 * (g & 1) + 8 * (g >> 1);
+#pragma unroll
+        for (int nt = 0; nt < NT16; nt += 2) {
+          const unsigned p00 = pack_bf16x2(v[nt][0], v[nt][1]), p01 = pack_bf16x2(v[nt][2], v[nt][3]);
+          const unsigned p10 = pack_bf16x2(v[nt + 1][0], v[nt + 1][1]), p11 = pack_bf16x2(v[nt + 1][2], v[nt + 1][3]);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(p00, p10, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(p01, p11, false, false);
+          *reinterpret_cast<uint4*>(Y + m * ldy + 16 * nt + wcol) = uint4{s0[0], s1[0], s0[1], s1[1]};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int nt = 0; nt < NT16; ++nt) {
+        const int n0 = nt * 16 + 4 * g;
+        if (n0 < N) store4(Y + m * ldy + n0, v[nt]);
+      }
     }
   }
 }
@@ -2298,6 +2331,8 @@ conv_skinny_kernel(const __bf16* __restrict__ X, int H, int W, int Cin, int KW, 
 template <typename TC>
 int launch_conv_skinny(const comet_conv_args& a, int64_t M, int OH, int OW, int K, hipStream_t s) {
   Epi e{a.bias, a.bias ? 1 : 0, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, 1.f, a.act, 0};
+  e.wide = a.cout % 32 == 0 && (uintptr_t)a.y % 16 == 0 && a.ldy % 8 == 0 && getenv("COMET_CONV_NO_WIDE") == nullptr;
+  COMET_CHECK_ARG(M + 64 < (1ll << 31), "comet_conv2d_nhwc (narrow): too many output pixels");
   int64_t blocks = cdiv(cdiv(M, 16), 4 * 8);
   if (blocks > 4096) blocks = 4096;
   const int nt = (int)(a.cout / 16), kc = (int)cdiv(K, 32);
