@@ -2276,22 +2276,17 @@ conv_skinny_kernel(const __bf16* __restrict__ X, int H, int W, int Cin, int KW, 
   // 16-B bf16 stores (epi.wide, host-checked: cout % 32 == 0, Y 16-B aligned, ldy % 8 == 0): channel
   // blocks nt, nt + 1 exchange lane-group halves by v_permlane16_swap so a lane stores 8 channels
   constexpr bool WIDE = std::is_same<TC, __bf16>::value && NT16 % 2 == 0;
-  bf16x8 xa[KC], xb[KC];
-  gather(wave * 16, xa);
-  for (int64_t m0 = wave * 16; m0 < M; m0 += nwaves * 16) {
-    const int64_t m = m0 + li;
-    const bool mok = m < M;
-    f32x4 acc[NT16];
+  auto mfmas = [&](const bf16x8 (&xc)[KC], f32x4 (&acc)[NT16]) {
 #pragma unroll
     for (int nt = 0; nt < NT16; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < KC; ++c)
 #pragma unroll
-      for (int nt = 0; nt < NT16; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt][c], xa[c], acc[nt], 0, 0, 0);
-    if (m0 + nwaves * 16 < M) gather(m0 + nwaves * 16, xb);
-#pragma unroll
-    for (int c = 0; c < KC; ++c) xa[c] = xb[c];
-    if (!mok) continue;
+      for (int nt = 0; nt < NT16; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[nt][c], xc[c], acc[nt], 0, 0, 0);
+  };
+  auto epilogue = [&](int64_t m0, const f32x4 (&acc)[NT16]) {
+    const int64_t m = m0 + li;
+    if (m >= M) return;
     float v[NT16][4];
 #pragma unroll
     for (int nt = 0; nt < NT16; ++nt) {
@@ -2325,6 +2320,33 @@ conv_skinny_kernel(const __bf16* __restrict__ X, int H, int W, int Cin, int KW, 
         if (n0 < N) store4(Y + m * ldy + n0, v[nt]);
       }
     }
+  };
+  const int64_t mstep = nwaves * 16;
+  bf16x8 xa[KC], xb[KC];
+  gather(wave * 16, xa);
+  if constexpr (KC >= 6) {
+    // long K (many taps): the next step's gather is issued before this step's MFMAs and two steps
+    // per trip swap the buffers, so its latency overlaps the MFMAs and the epilogue (3x3 s2 16^2:
+    // 418 -> 389 us; the short-K steps lose occupancy to the second buffer: gathered after the MFMAs)
+    for (int64_t m0 = wave * 16; m0 < M; m0 += 2 * mstep) {
+      f32x4 acc[NT16];
+      if (m0 + mstep < M) gather(m0 + mstep, xb);
+      mfmas(xa, acc);
+      epilogue(m0, acc);
+      if (m0 + mstep >= M) break;
+      if (m0 + 2 * mstep < M) gather(m0 + 2 * mstep, xa);
+      mfmas(xb, acc);
+      epilogue(m0 + mstep, acc);
+    }
+  } else {
+    for (int64_t m0 = wave * 16; m0 < M; m0 += mstep) {
+      f32x4 acc[NT16];
+      mfmas(xa, acc);
+      if (m0 + mstep < M) gather(m0 + mstep, xb);
+#pragma unroll
+      for (int c = 0; c < KC; ++c) xa[c] = xb[c];
+      epilogue(m0, acc);
+    }
   }
 }
 
@@ -2348,7 +2370,7 @@ int launch_conv_skinny(const comet_conv_args& a, int64_t M, int OH, int OW, int 
   } while (0)
   if (nt == 1) CSK_K(1); else if (nt == 2) CSK_K(2);
   else if (nt == 3) { if (kc <= 8) CSK_K(3); }
-  else { if (kc <= 8) CSK_K(4); }
+  else { if (kc <= 8) CSK_K(4); else if (kc <= 13) CSK(4, 13); }
 #undef CSK_K
 #undef CSK
   COMET_CHECK_LAUNCH("comet_conv2d_nhwc (narrow)");
@@ -2540,7 +2562,9 @@ int launch_conv(const comet_conv_args& a, hipStream_t s) {
   if (conv_rows_ok<TC>(a)) return launch_conv_rows<TC>(a, s);
   // narrow outputs: weights fit the registers (cout/16 x ceil(K/32) fragments <= 32)
   const int64_t kcs = cdiv(K, 32);
-  if (a.cout % 16 == 0 && a.cout <= 64 && (a.cout / 16) * kcs <= 32 && kcs <= 16 && M >= 16384 &&
+  // (and the BasicEncoder's 7x7 stem, cout 64 x K 392: 52 fragments, 208 registers at one wave per SIMD)
+  const bool stem = a.cout == 64 && kcs > 8 && kcs <= 13 && getenv("COMET_CONV_NO_STEM") == nullptr;
+  if (a.cout % 16 == 0 && a.cout <= 64 && ((a.cout / 16) * kcs <= 32 || stem) && kcs <= 16 && M >= 16384 &&
       (uintptr_t)a.y % (4 * sizeof(TC)) == 0 && a.ldy % 4 == 0 && getenv("COMET_CONV_NO_SKINNY") == nullptr &&
       (a.resid == nullptr || ((uintptr_t)a.resid % (4 * sizeof(TC)) == 0 && a.ldr % 4 == 0)))
     return launch_conv_skinny<TC>(a, M, (int)oh, (int)ow, (int)K, s);

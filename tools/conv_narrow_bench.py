@@ -19,6 +19,8 @@ from tile_bench import timed  # noqa: E402
 SHAPES = [  # (n, h, w, c, cout, k, stride, pad)
     (65536, 31, 31, 8, 32, 3, 2, 1), (65536, 16, 16, 32, 32, 3, 2, 1), (65536, 8, 8, 32, 32, 3, 1, 1),
     (65536, 16, 16, 32, 32, 1, 2, 0), (65536, 8, 8, 32, 32, 3, 2, 1), (65536, 4, 4, 32, 32, 3, 1, 1),
+    # the BasicEncoder's 7x7 stride-2 stem (3 channels padded to 8, frames halved to 256^2)
+    (128, 256, 256, 8, 64, 7, 2, 3),
 ]
 
 
