@@ -60,6 +60,45 @@ def free_port():
     return port
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def visible_gpu_count(kfd_nodes=KFD_NODES, dev_dri="/dev/dri"):
+    """GPUs this process could open, counted without any HIP call (the parent of the --gpus N
+    ranks must leave the device untouched, and torch.cuda.device_count() falls back to
+    hipGetDeviceCount when amdsmi is missing): KFD topology nodes with SIMDs (GPU agents) whose
+    render node /dev/dri/renderD<minor> is accessible (what the ROCm runtime enumerates; a container
+    sees every node in sysfs but only its own render devices), then capped by any
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES list. -> None when the
+    topology cannot be read (the caller refuses rather than guess)."""
+    try:
+        nodes = os.listdir(kfd_nodes)
+    except OSError:
+        return None
+    n = 0
+    for node in nodes:
+        props = {}
+        try:
+            with open(os.path.join(kfd_nodes, node, "properties")) as f:
+                for line in f:
+                    kv = line.split()
+                    if len(kv) == 2:
+                        props[kv[0]] = kv[1]
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue  # a CPU agent
+        minor = props.get("drm_render_minor")
+        if minor is None or not os.access(os.path.join(dev_dri, f"renderD{minor}"), os.R_OK | os.W_OK):
+            continue
+        n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def spawn_ranks(n):
     """One fresh process per GPU (the driver's `--gpus N` without torch.distributed.run). The
     children re-run this script with the rank environment a launcher would set; rank 0 prints the
@@ -273,10 +312,14 @@ def main():
         return 0
     launched = "WORLD_SIZE" in os.environ
     if not launched and args.gpus > 1:
-        # this process spawns the ranks; it never touches the GPU (device_count does not
-        # initialise HIP on this image), so the children start on a clean device
+        # this process spawns the ranks and never touches the GPU (no HIP call: visible_gpu_count
+        # reads sysfs), so the children start on a clean device
         if not args.launcher_check:
-            have = torch.cuda.device_count()
+            have = visible_gpu_count()
+            if have is None:
+                print(f"[bench] --gpus {args.gpus}: cannot count GPUs without initialising HIP ({KFD_NODES} "
+                      f"unreadable); refusing", file=sys.stderr, flush=True)
+                return 2
             if have < args.gpus:
                 print(f"[bench] --gpus {args.gpus} but only {have} GPU(s) visible; refusing to report a "
                       f"{have}-GPU run as {args.gpus}", file=sys.stderr, flush=True)

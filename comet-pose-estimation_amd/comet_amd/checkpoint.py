@@ -10,7 +10,8 @@
   save_state / load_state the accelerate.save_state(output_dir, safe_serialization=False) /
                           load_state directory the reference writes every ckpt_interval epochs and
                           auto-resumes from (train_e2epose2.py:92-113, 157-163, 185): the files
-                          pytorch_model.bin (unwrapped model state_dict), optimizer.bin,
+                          pytorch_model.bin (model state_dict; `module.` keys of a
+                          DDP run's file accepted on load), optimizer.bin,
                           scheduler.bin and random_states_<rank>.pkl (step, python / numpy / torch
                           CPU / torch device RNG states), all torch.save archives, as accelerate
                           1.x names and fills them
@@ -116,26 +117,33 @@ def _numpy_safe_globals():
 
 def save_state(output_dir, model, optimizer=None, scheduler=None, step=0, process_index=0):
     """accelerate.Accelerator.save_state(output_dir, safe_serialization=False) for one model /
-    optimizer / scheduler: pytorch_model.bin holds the unwrapped model's state_dict (no `module.`
-    prefix, as accelerate unwraps before saving)."""
+    optimizer / scheduler. pytorch_model.bin holds the model's state_dict without a `module.`
+    prefix (this build never wraps the model; accelerate 1.x itself saves
+    get_state_dict(model, unwrap=False), so the reference's multi-GPU runs write `module.` keys,
+    which load_state accepts). As accelerate does, only process 0 writes the model, optimizer and
+    scheduler files (accelerate.utils.save on the main process); every rank writes its own
+    random_states_<rank>.pkl. No barrier, as accelerate's save_state without automatic naming has
+    none: train_e2epose2.py:157-163 calls it from the main process alone."""
     os.makedirs(output_dir, exist_ok=True)
-    torch.save(_unwrap(model).state_dict(), os.path.join(output_dir, MODEL_FILE))
-    if optimizer is not None:
-        torch.save(optimizer.state_dict(), os.path.join(output_dir, OPTIMIZER_FILE))
-    if scheduler is not None:
-        torch.save(scheduler.state_dict(), os.path.join(output_dir, SCHEDULER_FILE))
+    if process_index == 0:
+        torch.save(_unwrap(model).state_dict(), os.path.join(output_dir, MODEL_FILE))
+        if optimizer is not None:
+            torch.save(optimizer.state_dict(), os.path.join(output_dir, OPTIMIZER_FILE))
+        if scheduler is not None:
+            torch.save(scheduler.state_dict(), os.path.join(output_dir, SCHEDULER_FILE))
     torch.save(_rng_states(step), os.path.join(output_dir, RNG_FILE.format(process_index)))
     return output_dir
 
 
 def load_state(input_dir, model, optimizer=None, scheduler=None, process_index=0, device=None, strict=True):
-    """accelerate.Accelerator.load_state(input_dir): model (strict), optimizer (state moved to the
-    params' device), scheduler, RNG states of this process. -> the saved step counter."""
+    """accelerate.Accelerator.load_state(input_dir): model (strict; a `module.` prefix written by
+    a DDP-wrapped reference run is stripped), optimizer (state moved to the params' device),
+    scheduler, RNG states of this process. -> the saved step counter."""
     if not os.path.isdir(input_dir):
         raise ValueError(f"Tried to find {input_dir} but folder does not exist")
     m = _unwrap(model)
     dev = device if device is not None else next(m.parameters()).device
-    m.load_state_dict(_load(os.path.join(input_dir, MODEL_FILE), dev), strict=strict)
+    m.load_state_dict(_with_prefix(_load(os.path.join(input_dir, MODEL_FILE), dev), False), strict=strict)
     if optimizer is not None:
         optimizer.load_state_dict(_load(os.path.join(input_dir, OPTIMIZER_FILE), dev))
     if scheduler is not None:

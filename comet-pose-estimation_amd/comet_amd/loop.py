@@ -24,6 +24,9 @@
                        with the reference's loader settings, host stage in the workers and the
                        crop / resize on the device in this process (DeviceLoader)
   train_fn             train_e2epose2.py:45-186
+  CsvLogger, test_fn   abl_ours.py:9-88, the evaluation entry point: eval loader (drop_last set
+                       on its batch sampler), load_model_weights2, one eval pass of
+                       train_or_eval_fn, one row in output_dir/test_results.csv
 """
 import gzip
 import json
@@ -181,23 +184,30 @@ class _BatchShard(torch.utils.data.Sampler):
     dispatch, split_batches=False); the tail that does not fill every rank is dropped so all
     ranks run the same number of steps."""
 
-    def __init__(self, batch_sampler, rank, world):
-        self.bs, self.rank, self.world = batch_sampler, rank, world
+    def __init__(self, batch_sampler, rank, world, even_batches=True):
+        self.bs, self.rank, self.world, self.even = batch_sampler, rank, world, even_batches
 
     def __len__(self):
-        return len(self.bs) // self.world
+        n = len(self.bs)
+        if self.even:
+            return n // self.world
+        return n // self.world + (1 if self.rank < n % self.world else 0)
 
     def __iter__(self):
-        n = len(self)
+        n = len(self.bs) // self.world if self.even else None
         for i, b in enumerate(self.bs):
-            if i // self.world >= n:
+            if n is not None and i // self.world >= n:
                 break
             if i % self.world == self.rank:
                 yield b
 
 
 class CometAccelerator:
-    def __init__(self, mixed_precision="no", device=None, bucket_mb=25):
+    """even_batches=False (abl_ours.py:28): the batches that do not fill every rank are kept, so
+    the last ranks may run one batch fewer, instead of being dropped (this build never pads by
+    repeating samples, so even_batches=True drops that tail)."""
+
+    def __init__(self, mixed_precision="no", device=None, bucket_mb=25, even_batches=True):
         import torch.distributed as dist
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
@@ -207,6 +217,7 @@ class CometAccelerator:
         self.device = torch.device(device)
         self.mixed_precision = mixed_precision
         self.bucket_mb = bucket_mb
+        self.even_batches = even_batches
         self.ddp = None
         self._optimizer = None
         self.step = 0
@@ -235,7 +246,8 @@ class CometAccelerator:
             return dl
         from .data import DeviceLoader
         inner = dl.loader if isinstance(dl, DeviceLoader) else dl
-        kw = dict(batch_sampler=_BatchShard(inner.batch_sampler, self.rank, self.world), num_workers=inner.num_workers,
+        kw = dict(batch_sampler=_BatchShard(inner.batch_sampler, self.rank, self.world, self.even_batches),
+                  num_workers=inner.num_workers,
                   collate_fn=inner.collate_fn, pin_memory=inner.pin_memory, worker_init_fn=inner.worker_init_fn,
                   generator=inner.generator)
         if inner.num_workers > 0:
@@ -247,8 +259,13 @@ class CometAccelerator:
         """accelerator.prepare(model, dataloader, optimizer, lr_scheduler) (train_e2epose2.py:83):
         model to the device, train loader sharded over ranks, gradient buckets over the
         optimizer's params (the camera predictor) when world > 1. The optimizer's own clip is
-        switched off: the loop clips through clip_grad_norm_ as the reference does."""
+        switched off: the loop clips through clip_grad_norm_ as the reference does. With world > 1
+        every parameter and buffer is broadcast from rank 0 first (what DDP's _sync_module_states
+        does when accelerate wraps the model): the ranks are seeded seed + rank, so their random
+        inits differ, and load_model_weights always leaves pose_branch.fc2 at its init."""
         model = model.to(self.device)
+        if self.world > 1:
+            self.sync_module_states(model)
         if optimizer is not None and hasattr(optimizer, "max_norm"):
             optimizer.max_norm = None
         self._optimizer = optimizer
@@ -257,6 +274,15 @@ class CometAccelerator:
             params = [p for g in optimizer.param_groups for p in g["params"]]
             self.ddp = GradBucketer(params, bucket_mb=self.bucket_mb)
         return model, self._shard(dataloader), optimizer, lr_scheduler
+
+    @staticmethod
+    @torch.no_grad()
+    def sync_module_states(model, src=0):
+        """Rank src's parameters and buffers to every rank, in state_dict order (one broadcast per
+        tensor; runs once, at prepare)."""
+        import torch.distributed as dist
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, src)
 
     def backward(self, loss):
         if self.ddp is not None:
@@ -482,4 +508,72 @@ def train_fn(cfg, data_root=None, eval_only=True, csv_log=True):
         if epoch != 0 and epoch % int(_get(cfg, "train.eval_interval", 1)) == 0:
             run_eval(epoch)
     acc.save_state(ckpt.checkpoint_path(exp_dir, epoch), model, optimizer, lr_scheduler)
+    return True
+
+
+# ------------------------------------------------------------------------------------------------
+class CsvLogger:
+    """abl_ours.py:9-22: header written once when the file is new, one DictWriter row per log()."""
+
+    def __init__(self, path, fieldnames):
+        import csv
+        self.path, self.fieldnames, self._csv = path, list(fieldnames), csv
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        if not os.path.exists(path):
+            with open(path, "w", newline="") as f:
+                csv.DictWriter(f, fieldnames=self.fieldnames).writeheader()
+
+    def log(self, row):
+        with open(self.path, "a", newline="") as f:
+            self._csv.DictWriter(f, fieldnames=self.fieldnames).writerow(row)
+
+
+def test_fn(cfg, data_root=None, sp=None):
+    """abl_ours.py:24-88, the evaluation entry point: accelerator with even_batches=False and the
+    config's mixed precision, seed (+ rank), output_dir/test_results.csv (fields epoch, it, mode +
+    TO_PLOT_METRICS), the eval loader with drop_last set on its batch sampler, the model from
+    cfg.MODEL, build_optimizer over the eval loader (the scheduler supplies the logged lr),
+    load_model_weights2 when train.resume_ckpt names a file, prepare, one eval pass of
+    train_or_eval_fn at epoch -1, then the eval averages + lr as one CSV row on the main process.
+    -> True. Differences: the model is always on the accelerator's device (the reference's
+    device_placement=False leaves it where load_model_weights2 put it, on the device when a
+    checkpoint is given), and `data_root` / cfg.data_root / $COMET_DATA_ROOT names the AMD
+    dataset directory the reference hard-codes."""
+    from .config import instantiate
+    from .train import build_optimizer
+    acc = CometAccelerator(mixed_precision=_get(cfg, "mixed_precision", "no"), even_batches=False)
+    set_seed_and_print(int(_get(cfg, "seed", 0)))
+    logger = None
+    csv_path = os.path.join(_get(cfg, "output_dir", "."), "test_results.csv")
+    if acc.is_main_process:
+        logger = CsvLogger(csv_path, ["epoch", "it", "mode"] + list(TO_PLOT_METRICS))
+        acc.print(f"Test results will be saved to {csv_path}")
+    _, _, _, eval_dataloader = build_dataset(cfg, data_root, acc.device)
+    inner = getattr(eval_dataloader, "loader", eval_dataloader)
+    if getattr(inner, "batch_sampler", None) is not None:
+        inner.batch_sampler.drop_last = True
+    acc.print(f"Length of eval dataloader: {len(eval_dataloader)}")
+    try:
+        model = instantiate(cfg["MODEL"], _recursive_=False, cfg=cfg)
+    except Exception as e:  # abl_ours.py:44-47
+        raise RuntimeError(f"Failed to instantiate model: {e}")
+    optimizer, lr_scheduler = build_optimizer(cfg, model, eval_dataloader)
+    start_epoch = 0
+    resume = _get(cfg, "train.resume_ckpt", "")
+    if resume and os.path.isfile(resume):
+        acc.print(f"Loading weights from specific file: {resume}")
+        model = ckpt.load_model_weights2(model, resume, acc.device, _get(cfg, "relax_load", False))
+    model, eval_dataloader, optimizer, lr_scheduler = acc.prepare(model, eval_dataloader, optimizer, lr_scheduler)
+    acc.print(f"---------- Start Testing (Model Epoch: {start_epoch - 1}) ----------")
+    stats = Stats(TO_PLOT_METRICS)
+    lr = lr_scheduler.get_last_lr()[0]
+    train_or_eval_fn(model, eval_dataloader, cfg, optimizer, stats, acc, lr_scheduler, training=False,
+                     epoch=start_epoch - 1, sp=sp)
+    stats.update({"lr": lr}, stat_set="eval")
+    d = stats.get_epoch_averages()["eval"]
+    if acc.is_main_process:
+        row = {"epoch": d.get("epoch", start_epoch - 1), "it": d.get("it", 0), "mode": "eval"}
+        row.update({k: d.get(k, "") for k in TO_PLOT_METRICS})
+        logger.log(row)
+        print(f"Test finished. Results saved to {csv_path}")
     return True

@@ -67,7 +67,11 @@ class CometAdamW(torch.optim.Optimizer):
     def clip_grad_norm_(self, max_norm):
         """accelerator.clip_grad_norm_(params, max_norm) of the reference loop
         (train_eval_func_new_cp5.py:797): the total gradient norm now (device scalar, no sync);
-        the scaling itself is applied inside the next step()'s AdamW kernel."""
+        the scaling itself is applied inside the next step()'s AdamW kernel, so between this call
+        and step() p.grad still holds the unclipped gradient (unlike accelerate, which scales in
+        place); the stored norm belongs to the gradients of this moment and is dropped by the next
+        step() whatever path it takes. Code that changes the gradients in between (accumulation,
+        another backward) must call clip_grad_norm_ again."""
         sq = self.grad_sqnorm()
         self._pending = (float(max_norm), sq)
         return sq.sqrt()
@@ -126,10 +130,10 @@ class CometAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        pend, self._pending = self._pending, None  # consumed on every path, the early return too
         ps = self._with_grad()
         if not ps:
             return loss
-        pend, self._pending = self._pending, None
         if max_norm is None and pend is not None:
             max_norm, sq = pend
         else:

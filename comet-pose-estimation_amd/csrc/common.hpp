@@ -150,8 +150,9 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
 // q is a degree-6 fit of log2 Phi(-a) on a = min(|x|, 6) (Phi(-6) = 9.9e-10), weighted by a Phi(-a)
 // so the GELU error is even: |err| <= 2.8e-7 over the f32 line (fit and check: tools/gelu_fit.py;
 // the Abramowitz-Stegun 7.1.26 erf form used before: 4.6e-7). One v_exp_f32 and 9 VALU operations
-// against two transcendentals and ~15: the GELU GEMM epilogues are VALU-bound. Non-finite inputs stay
-// non-finite (+inf -> nan, -inf -> -inf; the erf form gives inf / nan).
+// against two transcendentals and ~15: the GELU GEMM epilogues are VALU-bound. Non-finite inputs give
+// NaN, as torch's f32 GELU does (fmaxf / fminf drop a NaN operand, so the relu term is fma(x, 0, relu):
+// x * 0 is 0 for finite x and NaN for NaN / +-inf; one more fma per value, one packed fma per pair).
 // The last step multiplies by the clamped a rather than |x|: for |x| > 6 the term is below 6e-9 either
 // way (and nearer the true GELU with a); the pair form below then needs no second |x| register.
 __device__ __forceinline__ float gelu_erf(float x) {
@@ -162,7 +163,7 @@ __device__ __forceinline__ float gelu_erf(float x) {
   q = fmaf(q, a, -4.587708414e-01f);
   q = fmaf(q, a, -1.151201725e+00f);
   q = fmaf(q, a, -9.999930859e-01f);
-  return fmaf(-a, __builtin_amdgcn_exp2f(q), fmaxf(x, 0.f));
+  return fmaf(-a, __builtin_amdgcn_exp2f(q), fmaf(x, 0.f, fmaxf(x, 0.f)));
 }
 // The same GELU on two values with packed f32 math (v_pk_fma_f32: the six polynomial steps and the
 // final fma issue once per pair): 13 VALU instructions per pair instead of 21, bit-identical to
@@ -177,7 +178,8 @@ __device__ __forceinline__ void gelu_erf2(float& x0, float& x1) {
   q = __builtin_elementwise_fma(q, a, (f32x2_t)(-1.151201725e+00f));
   q = __builtin_elementwise_fma(q, a, (f32x2_t)(-9.999930859e-01f));
   const f32x2_t e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
-  const f32x2_t r = {fmaxf(x0, 0.f), fmaxf(x1, 0.f)};
+  const f32x2_t xv = {x0, x1};
+  const f32x2_t r = __builtin_elementwise_fma(xv, (f32x2_t)(0.f), (f32x2_t){fmaxf(x0, 0.f), fmaxf(x1, 0.f)});
   const f32x2_t o = __builtin_elementwise_fma(-a, e, r);
   x0 = o.x;
   x1 = o.y;

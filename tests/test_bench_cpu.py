@@ -33,14 +33,60 @@ def test_launcher_spawns_two_ranks_and_reduces():
     assert j["n_gpus"] == 2 and j["backend"] == "gloo" and j["reduced"] is True and j["buckets"] > 1
 
 
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_under_test", BENCH)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
 def test_refuses_more_gpus_than_visible():
     r = _run(["--gpus", "2", "--no-cpu-baseline"])
-    import torch
-    if torch.cuda.device_count() >= 2:  # pragma: no cover - a multi-GPU host
+    b = _bench_module()
+    have = b.visible_gpu_count()
+    if have is not None and have >= 2:  # pragma: no cover - a multi-GPU host
         return
     assert r.returncode == 2
     assert "refusing" in r.stderr
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_parent_counts_gpus_without_hip(tmp_path, monkeypatch):
+    """The --gpus N parent never calls into HIP: torch's own device counters are made to raise,
+    amdsmi is hidden, and the count comes from a fake KFD topology (a CPU node, two GPU nodes of
+    which one render device is accessible), capped by *_VISIBLE_DEVICES; an unreadable topology
+    makes main() refuse (exit 2) instead of falling back to hipGetDeviceCount."""
+    import torch
+    b = _bench_module()
+
+    def boom(*a, **k):
+        raise AssertionError("HIP device count called in the --gpus N parent")
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom, raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.setitem(sys.modules, "amdsmi", None)
+    nodes, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    for i, (simd, minor) in enumerate([(0, None), (1024, 128), (1024, 129), (1024, 130)]):
+        d = nodes / str(i)
+        d.mkdir(parents=True)
+        lines = [f"simd_count {simd}"] + ([f"drm_render_minor {minor}"] if minor is not None else [])
+        (d / "properties").write_text("\n".join(lines) + "\n")
+    for minor in (128, 130):
+        (dri / f"renderD{minor}").write_text("")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert b.visible_gpu_count(str(nodes), str(dri)) == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0")
+    assert b.visible_gpu_count(str(nodes), str(dri)) == 1
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    assert b.visible_gpu_count(str(tmp_path / "missing"), str(dri)) is None
+    monkeypatch.setattr(b, "visible_gpu_count", lambda *a, **k: None)
+    monkeypatch.setattr(b, "spawn_ranks", boom)
+    monkeypatch.setattr(sys, "argv", [BENCH, "--gpus", "2", "--no-cpu-baseline"])
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    assert b.main() == 2
 
 
 def test_world_size_must_match_gpus():

@@ -155,6 +155,50 @@ def test_checkpoint_directory_round_trip(tmp_path):
     assert C.load_tdict(path) == {"epoch": 7, "cfg": {"seed": 0, "train": {"lr": 1e-5}}}
 
 
+def test_load_state_accepts_ddp_prefixed_model_file(tmp_path):
+    """accelerate 1.x saves get_state_dict(model, unwrap=False): a reference run under DDP writes
+    `module.`-prefixed keys into pytorch_model.bin; load_state strips them for the plain model."""
+    from collections import OrderedDict
+    from comet_amd import checkpoint as C
+    torch.manual_seed(0)
+    net = _Net()
+    path = str(tmp_path / "ckpt_000003")
+    os.makedirs(path)
+    torch.save(OrderedDict(("module." + k, v) for k, v in net.state_dict().items()),
+               os.path.join(path, C.MODEL_FILE))
+    torch.manual_seed(1)
+    net2 = _Net()
+    C.load_state(path, net2)
+    for (k, a), b in zip(net.state_dict().items(), net2.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
+def test_save_state_other_ranks_write_only_their_rng_file(tmp_path):
+    """accelerate.utils.save writes the model / optimizer / scheduler archives on the main process
+    only; every rank writes random_states_<rank>.pkl (no torn concurrent writes of one file)."""
+    from comet_amd import checkpoint as C
+    from comet_amd.train import CometAdamW
+    net = _Net()
+    opt = CometAdamW(net.camera_predictor.parameters(), lr=1e-3)
+    path = str(tmp_path / "ckpt_000001")
+    C.save_state(path, net, opt, None, step=3, process_index=1)
+    assert sorted(os.listdir(path)) == ["random_states_1.pkl"]
+    C.save_state(path, net, opt, None, step=3, process_index=0)
+    assert sorted(os.listdir(path)) == ["optimizer.bin", "pytorch_model.bin", "random_states_0.pkl",
+                                        "random_states_1.pkl"]
+
+
+def test_step_drops_pending_clip_on_every_path():
+    """clip_grad_norm_'s stored (max_norm, norm) is consumed by the next step() even when that
+    step returns early because no parameter has a gradient, so it never leaks into a later step."""
+    from comet_amd.train import CometAdamW
+    net = _Net()
+    opt = CometAdamW(net.camera_predictor.parameters(), lr=1e-3)
+    opt._pending = (1.0, torch.ones(1))
+    opt.step()  # no gradients: early return
+    assert opt._pending is None
+
+
 def test_tdict_refuses_objects(tmp_path):
     from comet_amd.checkpoint import load_tdict
 
@@ -185,6 +229,27 @@ def test_batch_shard_partitions_batches():
     assert all(len(s) == len(_BatchShard(bs, 0, 4)) == 2 for s in shards)
     flat = [tuple(b) for s in shards for b in s]
     assert len(set(flat)) == 8 and set(flat) <= {tuple(b) for b in bs}
+
+
+def test_batch_shard_uneven_keeps_tail():
+    """even_batches=False (abl_ours.py:28): 5 batches over 2 ranks -> 3 + 2, nothing dropped."""
+    from comet_amd.loop import _BatchShard
+    bs = [[i] for i in range(5)]
+    r0, r1 = _BatchShard(bs, 0, 2, False), _BatchShard(bs, 1, 2, False)
+    assert list(r0) == [[0], [2], [4]] and len(r0) == 3
+    assert list(r1) == [[1], [3]] and len(r1) == 2
+
+
+def test_csv_logger(tmp_path):
+    """abl_ours.py:9-22: header once, then one row per log(); reopening appends."""
+    import csv
+    from comet_amd.loop import CsvLogger
+    p = str(tmp_path / "out" / "test_results.csv")
+    CsvLogger(p, ["epoch", "it", "mode"]).log({"epoch": -1, "it": 3, "mode": "eval"})
+    CsvLogger(p, ["epoch", "it", "mode"]).log({"epoch": 0, "it": 1, "mode": "eval"})
+    with open(p) as f:
+        rows = list(csv.DictReader(f))
+    assert rows == [{"epoch": "-1", "it": "3", "mode": "eval"}, {"epoch": "0", "it": "1", "mode": "eval"}]
 
 
 def test_stats_round_trip(tmp_path):

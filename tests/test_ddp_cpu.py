@@ -154,3 +154,48 @@ def test_unused_param_in_first_bucket_does_not_delay_allreduce():
                     assert g is None, k
                 else:
                     torch.testing.assert_close(torch.from_numpy(g), exp[step][k], rtol=1e-5, atol=1e-6)
+
+
+def _prepare_worker(rank, world, port, q, paths):
+    import sys
+    sys.path[:0] = paths
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from comet_amd.loop import CometAccelerator
+        torch.manual_seed(1000 + rank)  # seed + rank, as set_seed_and_print(device_specific=True)
+        net = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.BatchNorm1d(32), torch.nn.Linear(32, 4))
+        net[1].running_mean.normal_()
+        before = {k: v.clone() for k, v in net.state_dict().items()}
+        opt = torch.optim.SGD(net.parameters(), lr=0.1)
+        acc = CometAccelerator(device="cpu")
+        net, _, opt, _ = acc.prepare(net, None, opt, None)
+        q.put((rank, {k: v.numpy().copy() for k, v in before.items()},
+               {k: v.detach().numpy().copy() for k, v in net.state_dict().items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_prepare_broadcasts_rank0_weights():
+    """CometAccelerator.prepare with world > 1 starts every rank from rank 0's parameters and
+    buffers (DDP's _sync_module_states under accelerate.prepare), whatever each rank's seed."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_prepare_worker, args=(r, world, port, q, [ROOT, PKG])) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, before, after = q.get(timeout=120)
+        res[rank] = (before, after)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert not np.array_equal(res[0][0]["0.weight"], res[1][0]["0.weight"])  # the inits differed
+    for k in res[0][1]:
+        assert np.array_equal(res[0][1][k], res[0][0][k]), k     # rank 0 kept its own
+        assert np.array_equal(res[1][1][k], res[0][0][k]), k     # rank 1 got rank 0's

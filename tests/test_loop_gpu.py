@@ -69,3 +69,37 @@ def test_train_or_eval_fn_and_checkpoint_resume(tmp_path):
     assert all(s2[i]["step"].device.type == "cpu" for i in s2)
     assert sched2.get_last_lr() == sched.get_last_lr()
     assert Stats.load(os.path.join(last, "train_stats.jgz")).get_epoch_averages() == stats.get_epoch_averages()
+
+
+def test_abl_ours_test_fn_end_to_end(tmp_path):
+    """abl_ours.py:24-88 through comet_amd.loop.test_fn: the AMD_eval loader over an on-disk
+    YTDataset, drop_last on its batch sampler, load_model_weights2 of a checkpoint file, one
+    bf16 eval pass of train_or_eval_fn with SuperPoint keypoint tracks, and one row of
+    output_dir/test_results.csv with the reference's fields."""
+    import csv
+    from comet_amd import loop
+    from comet_amd.config import instantiate, load_config
+    root = tmp_path / "AMD"
+    yt_fixture.make_dataset(str(root / "AMD_eval"))
+    cfg = load_config(**{"train.track_num": 64, "train.img_size": 128, "seqlen": 4})
+    torch.manual_seed(3)
+    ref_model = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg)
+    wpath = str(tmp_path / "weights.bin")
+    torch.save(ref_model.state_dict(), wpath)
+    cfg["track_by_spsg"] = True
+    cfg["output_dir"] = str(tmp_path / "abl_ours_eval_fold")
+    cfg["train"]["dataset"] = "AMD_eval"
+    cfg["train"]["num_workers"] = 2
+    cfg["train"]["resume_ckpt"] = wpath
+    cfg["train"]["eval_print_interval"] = 1
+    assert loop.test_fn(cfg, data_root=str(root)) is True
+    with open(tmp_path / "abl_ours_eval_fold" / "test_results.csv") as f:
+        rows = list(csv.DictReader(f))
+    assert len(rows) == 1
+    r = rows[0]
+    assert list(r.keys()) == ["epoch", "it", "mode"] + list(loop.TO_PLOT_METRICS)
+    assert r["mode"] == "eval" and int(r["epoch"]) == -1 and int(r["it"]) == 1   # two sequences
+    for k in ("Auc_30", "R_avg", "T_avg", "acc@5deg_x", "lr"):
+        v = float(r[k])
+        assert v == v, k   # logged and not NaN
+    assert float(r["lr"]) == pytest.approx(cfg["train"]["lr"])   # warmup_ratio 0: the base lr at step 0

@@ -196,6 +196,36 @@ def test_gemm_gelu_epilogue_precision(mnk):
     assert torch.isfinite(out).all()
 
 
+@pytest.mark.parametrize("mnk,dtype", [((257, 384, 64), torch.float32), ((8192, 1536, 384), torch.bfloat16)])
+def test_gelu_non_finite_propagates(mnk, dtype):
+    """NaN / +inf / -inf pre-activations give NaN through the GELU GEMM epilogue (the persistent
+    kernel's bf16 pairs for the second shape) and comet_act_fwd, as torch's f32 GELU does
+    (F.gelu(inf) = F.gelu(-inf) = nan on the CPU); finite columns are untouched."""
+    ops = _ops()
+    M, N, K = mnk
+    x = _rand(M, K, dtype=dtype, seed=7)
+    w = _rand(N, K, dtype=dtype, seed=8, scale=0.02)
+    b = torch.linspace(-3, 3, N)
+    bad_cols = {5: float("nan"), 6: float("inf"), 7: float("-inf"), N - 2: float("nan"), N - 1: float("-inf")}
+    for c, v in bad_cols.items():
+        b[c] = v
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    ops.linear(x.to(DEV), w.to(DEV), bias=b.to(DEV), act=1, out=out)
+    o = out.float().cpu()
+    cols = torch.tensor(sorted(bad_cols))
+    assert torch.isnan(o[:, cols]).all(), "GELU epilogue hid a non-finite pre-activation"
+    keep = torch.ones(N, dtype=torch.bool)
+    keep[cols] = False
+    assert torch.isfinite(o[:, keep]).all()
+    v = torch.tensor([float("nan"), float("inf"), float("-inf"), -50.0, 0.0, 2.0] * 64)
+    for dt_ in (torch.float32, torch.bfloat16):
+        y = ops.act_fwd(1, v.to(DEV, dt_)).float().cpu()
+        ref = F.gelu(v.to(dt_).float())
+        assert torch.isnan(y[:: 6]).all() and torch.isnan(y[1:: 6]).all() and torch.isnan(y[2:: 6]).all()
+        fin = torch.isfinite(ref)
+        assert torch.allclose(y[fin], ref[fin], atol=1e-2 if dt_ == torch.bfloat16 else 1e-6)
+
+
 def test_gemm_batched_strided():
     ops = _ops()
     # per (b, h): C = Q_bh K_bh^T with q/k packed [B, L, 3, H, D]
