@@ -243,8 +243,13 @@ class CameraPredictor(nn.Module):
         # ---- T_F ----
         if self.USE_TIME:
             rgb_feat = F.add_rows(rgb_feat, self._table("1d", S, C, rgb_feat.device), S)
-            for blk in self.trunk:
-                rgb_feat = blk(rgb_feat)
+            # the trunk runs in f32 whatever the compute dtype: its attention spans the T = 16 frames
+            # of one sequence, whose softmax backward cancels (dS = P (dP - delta) over nearly uniform
+            # P), so bf16 operands cost the q-projection gradient several % (the reference's own bf16
+            # autocast run: 2.9 %; tests/test_headline_gpu.py). 0.9 of the 7,477 GFLOP per sequence.
+            with F.precision(torch.float32):
+                for blk in self.trunk:
+                    rgb_feat = blk(rgb_feat)
         if self.SINGLE_HEAD:
             return self._single_head(rgb_feat, gt_cameras, B, S)
         gt_enc = None

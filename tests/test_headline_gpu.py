@@ -174,23 +174,20 @@ def test_headline_bf16_end_to_end_B2(setup, gold):
 def test_headline_bf16_camera_head_fwd_bwd(setup, gold, monkeypatch):
     """The product's training precision (bf16 operands, f32 accumulation / residual stream) through
     the camera head's forward AND backward at the headline size, on the reference's own stage
-    inputs, against the reference's bf16-autocast head fwd+bwd (tools/gen_golden.py
-    --headline-bf16-head). This runs the kernels the bench times for the backward: the bf16 flash
-    attention backward (dK/dV and dQ kernels, D=96), the 256-row split-K / ragged-K weight-gradient
-    GEMMs (K = 16 x 577 tokens), the bf16 LayerNorm backward and the activation-gradient column sums.
+    inputs. This runs the kernels the bench times for the backward: the bf16 flash attention
+    backward (dK/dV and dQ kernels, D=96), the 256-row split-K / ragged-K weight-gradient GEMMs
+    (K = 16 x 577 tokens), the bf16 LayerNorm backward and the activation-gradient column sums.
 
-    Tolerance: each of the 169 gradient norms is compared with the reference's bf16 norm allowing 2e-2
-    of the fp32 norm plus twice the reference's own bf16 deviation (|ref_bf16 - ref_fp32|): some head
-    gradients (fc_depth, confidence_attention, traj_encoder) move by O(1) between the reference's own
-    fp32 and bf16 runs, while ours stay within ~0.3 % of fp32. Selected gradient slices: relative
-    Frobenius error against the reference fp32 within 3e-2, or twice the reference bf16's own, or twice
-    the slice's rounding-order noise floor: the same head rerun with the camera trunk's split-K GEMMs
-    unsplit (identical math; only the f32 summation order, hence which bf16 roundings flip by one
-    ulp, changes) -- the 48 q-rows of trunk.0's in_proj gradient sit behind the softmax backward's
-    cancellation (dS = P (dP - delta) over T = 16 nearly uniform keys) and move by several % between
-    the two orders, as the reference's own bf16 run moves them by 2.9 % against its fp32.
-    Pose encoding: 1e-2 against the reference fp32 (north-star tolerance) and within 1e-2 + the
-    reference's bf16 deviation against its bf16 output, as the forward test."""
+    Every assertion is against the reference's FP32 head fwd+bwd (tools/gen_golden.py --headline):
+      * pose encoding (uvz, quaternion) within 1e-2 (north-star tolerance);
+      * each of the 169 gradient norms within 2e-2 of the reference fp32 norm (no allowance for the
+        reference's own bf16 deviation, which reaches O(1) for fc_depth / confidence_attention /
+        traj_encoder: those gradients are held to the fp32 norm like every other);
+      * each selected gradient slice by relative Frobenius error within 3e-2, for the product's
+        kernel plan AND for the same head rerun with the camera trunk's split-K GEMMs unsplit
+        (COMET_GEMM_NO_SMALLSPLIT: identical math, another f32 summation order).
+    The reference's bf16-autocast run (tools/gen_golden.py --headline-bf16-head) is printed beside
+    each figure as a diagnostic only."""
     from comet_amd import functional as F
     model, cfg, img, tracks, gt = setup
     cp = model.camera_predictor
@@ -207,25 +204,22 @@ def test_headline_bf16_camera_head_fwd_bwd(setup, gold, monkeypatch):
     ref16, ref32 = gold["head_bf16h_pred_pose_enc"], gold["head_pred_pose_enc"]
     close(enc[:, :3], ref32[:, :3], 0, 1e-2, "uvz (bf16 head vs reference fp32)")
     close(enc[:, 3:], ref32[:, 3:], 0, 1e-2, "quaternion (bf16 head vs reference fp32)")
-    e16 = np.abs(enc - ref16)
-    print(f"pose enc: max |ours - reference bf16| {e16.max():.3e}")
-    assert (e16 <= 1e-2 + np.abs(ref16 - ref32)).all()
-    close(out["loss"].reshape(1), gold["head_bf16h_loss"], 1e-2, 1e-3, "loss (bf16 head)")
+    print(f"pose enc: max |ours - reference bf16| {np.abs(enc - ref16).max():.3e}, "
+          f"|reference bf16 - reference fp32| {np.abs(ref16 - ref32).max():.3e} (diagnostic)")
+    close(out["loss"].reshape(1), gold["head_loss"], 1e-2, 1e-3, "loss (bf16 head vs reference fp32)")
     named = dict(cp.named_parameters())
     names = [str(k) for k in gold["head_grad_names"]]
     assert all(named[k].grad is not None for k in names)
     norms = np.array([named[k].grad.double().norm().item() for k in names])
     n16, n32 = gold["head_bf16h_grad_norms"], gold["head_grad_norms"]
-    allow = 2e-2 * n32 + 2 * np.abs(n16 - n32) + 1e-6
-    err = np.abs(norms - n16)
-    tight = np.abs(n16 - n32) <= 1e-2 * n32
-    print(f"169 gradient norms: max rel err vs reference bf16 {np.max(err / n16):.3e}; "
-          f"{int(tight.sum())} params where the reference's bf16 is within 1e-2 of its fp32: max rel err there "
-          f"{np.max((err / n32)[tight]):.3e}")
-    for i, k in enumerate(names):
-        if k.startswith("trunk.") or err[i] > 5e-3 * n32[i]:
-            print(f"  {k}: ours {norms[i]:.6e} ref bf16 {n16[i]:.6e} ref fp32 {n32[i]:.6e}")
-    bad = [(names[i], norms[i], n16[i], n32[i]) for i in np.nonzero(err > allow)[0]]
+    rel = np.abs(norms - n32) / n32
+    rel16 = np.abs(n16 - n32) / n32
+    order = np.argsort(-rel)
+    print(f"169 gradient norms vs reference fp32: max rel err {rel.max():.3e} (reference bf16: {rel16.max():.3e})")
+    for i in order[:12]:
+        print(f"  {names[i]}: ours {norms[i]:.6e} ref fp32 {n32[i]:.6e} (rel {rel[i]:.2e}); "
+              f"ref bf16 {n16[i]:.6e} (rel {rel16[i]:.2e})")
+    bad = [(names[i], norms[i], n32[i]) for i in np.nonzero(np.abs(norms - n32) > 2e-2 * n32 + 1e-6)[0]]
     assert not bad, bad[:8]
     slices = [k[len("head_bf16h_grad_full."):] for k in gold if k.startswith("head_bf16h_grad_full.")]
 
@@ -234,7 +228,7 @@ def test_headline_bf16_camera_head_fwd_bwd(setup, gold, monkeypatch):
         return g.reshape(named[name].shape[0], -1)[:rows]
 
     got = {n: grab(n, gold["head_bf16h_grad_full." + n].shape[0]) for n in slices}
-    # rounding-order noise floor: rerun with the split-K GEMMs unsplit (COMET_GEMM_NO_SMALLSPLIT)
+    # the same head with the split-K GEMMs unsplit: another summation order, same bound
     model.zero_grad(set_to_none=True)
     monkeypatch.setenv("COMET_GEMM_NO_SMALLSPLIT", "1")
     with F.precision(torch.bfloat16):
@@ -249,14 +243,75 @@ def test_headline_bf16_camera_head_fwd_bwd(setup, gold, monkeypatch):
     for name in slices:
         g16, g32 = gold["head_bf16h_grad_full." + name], gold["head_fp32h_grad_full." + name]
         g, g2 = got[name].reshape(g16.shape), alt[name].reshape(g16.shape)
-        # aggregate (Frobenius) relative error against the reference fp32 gradient
-        e_ours, e_ref = fro(g - g32) / fro(g32), fro(g16 - g32) / fro(g32)
-        e_alt, e_noise = fro(g2 - g32) / fro(g32), fro(g - g2) / fro(g32)
-        print(f"{name}: |ours - ref fp32|_F / |ref fp32|_F {e_ours:.3e} (unsplit order {e_alt:.3e}, "
-              f"order noise {e_noise:.3e}, reference bf16 {e_ref:.3e}); "
-              f"max-element |ours - ref fp32| / max|ref| {np.abs(g - g32).max() / np.abs(g32).max():.3e}")
-        bound = max(3e-2, 2 * e_ref, 2 * e_noise)
-        if e_ours > bound or e_alt > bound:
-            fails.append(name)
+        e_ours, e_alt, e_ref = fro(g - g32) / fro(g32), fro(g2 - g32) / fro(g32), fro(g16 - g32) / fro(g32)
+        print(f"{name}: |ours - ref fp32|_F / |ref fp32|_F {e_ours:.3e} (unsplit order {e_alt:.3e}; "
+              f"reference bf16 {e_ref:.3e}, diagnostic)")
+        if e_ours > 3e-2 or e_alt > 3e-2:
+            fails.append((name, e_ours, e_alt))
     assert not fails, fails
     model.zero_grad(set_to_none=True)
+
+
+def test_bench_batch_B8_sequences_independent_of_batch():
+    """BASELINE configs[2]'s exact step shape -- B=8, T=16, 512x512, N=512, bf16, forward AND
+    backward -- the batch the bench times (at B=8 the head and DINOv2 GEMMs run M ~ 73,856 rows,
+    so the persistent GEMM's tile plans of the bench run here). Property (sequences are
+    independent; loss = mean over sequences): every sequence's pose encoding
+    of the B=8 run equals the same sequence run alone (B=1) within 1e-2, and the B=8 camera-head
+    gradients equal the mean of the eight B=1 gradients -- 169 norms within 2e-2, selected tensors
+    by relative Frobenius error within 3e-2 (bf16; B=8 and B=1 take different GEMM tilings and
+    split-K plans, so the f32 summation orders differ)."""
+    from comet_amd import functional as F
+    from comet_amd.config import instantiate, load_config
+    from oracle import prng
+    from oracle.weights import comet_shapes
+    cfg = load_config()
+    torch.manual_seed(0)
+    model = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg)
+    model.load_state_dict(prng.make_state_dict(0, comet_shapes()), strict=True)
+    model = model.cuda()
+    cp = model.camera_predictor
+    B, T, S, N = 8, 16, 512, 512
+    img, tracks, gt = prng.synthetic_batch(41, B, T, S, S, N)
+    img, tracks = img.cuda(), tracks.cuda()
+    sub = lambda g, b: {k: (v[b * T:(b + 1) * T] if k != "ratio" else v) for k, v in g.items()}  # noqa: E731
+    params = [(k, p) for k, p in cp.named_parameters() if p.requires_grad]
+
+    def run(x, tr, g):
+        model.zero_grad(set_to_none=True)
+        with F.precision(torch.bfloat16):
+            out = model(x, gt_cameras=_cams(g), training=True, tracks=tr)
+            out["loss"].backward()
+        torch.cuda.synchronize()
+        return out["pred_pose_enc"].detach().float().cpu()
+
+    enc8 = run(img, tracks, gt).reshape(B, T, 7)
+    g8 = {k: p.grad.detach().clone() for k, p in params if p.grad is not None}
+    acc = {k: torch.zeros_like(v, dtype=torch.float64) for k, v in g8.items()}
+    worst_enc = 0.0
+    for b in range(B):
+        e1 = run(img[b:b + 1], tracks[b:b + 1], sub(gt, b)).reshape(T, 7)
+        d = (e1 - enc8[b]).abs().max().item()
+        worst_enc = max(worst_enc, d)
+        print(f"sequence {b}: pose enc max |B=8 - B=1| {d:.3e}")
+        assert d < 1e-2, (b, d)
+        for k, p in params:
+            if k in acc:
+                assert p.grad is not None, k
+                acc[k] += p.grad.double() / B
+    model.zero_grad(set_to_none=True)
+    assert torch.isfinite(enc8).all()
+    rels = []
+    for k, g in g8.items():
+        n8, nm = g.double().norm().item(), acc[k].norm().item()
+        rels.append((abs(n8 - nm) / max(nm, 1e-30), k, n8, nm))
+        assert abs(n8 - nm) <= 2e-2 * nm + 1e-6, (k, n8, nm)
+    rels.sort(reverse=True)
+    print(f"{len(g8)} gradient norms, B=8 vs mean of B=1: worst {rels[:4]}; pose enc worst {worst_enc:.3e}")
+    for k in ("fc_depth.weight", "pose_token", "self_att.0.attn.in_proj_weight", "cross_att.3.mlp.fc1.weight",
+              "trunk.0.attn.in_proj_weight", "traj_encoder.mlp.0.weight", "confidence_attention.0.weight"):
+        if k not in g8:
+            continue
+        e = ((g8[k].double() - acc[k]).norm() / acc[k].norm()).item()
+        print(f"{k}: |B=8 - mean B=1|_F / |mean B=1|_F {e:.3e}")
+        assert e < 3e-2, (k, e)

@@ -98,7 +98,9 @@ def test_abl_ours_test_fn_end_to_end(tmp_path):
     assert len(rows) == 1
     r = rows[0]
     assert list(r.keys()) == ["epoch", "it", "mode"] + list(loop.TO_PLOT_METRICS)
-    assert r["mode"] == "eval" and int(r["epoch"]) == -1 and int(r["it"]) == 1   # two sequences
+    from comet_amd.data import YTDataset
+    n = len(YTDataset(str(root / "AMD_eval"), crop_size=[128, 128], seq_len=4, split="valid"))
+    assert r["mode"] == "eval" and int(r["epoch"]) == -1 and int(r["it"]) == n - 1   # one iteration per sample
     for k in ("Auc_30", "R_avg", "T_avg", "acc@5deg_x", "lr"):
         v = float(r[k])
         assert v == v, k   # logged and not NaN
