@@ -33,7 +33,6 @@ import json
 import os
 import random
 import time
-from contextlib import nullcontext
 
 import numpy as np
 import torch
@@ -235,11 +234,14 @@ class CometAccelerator:
             print(*a, **k)
 
     def autocast(self):
+        """mixed_precision "bf16": bf16 operands (accelerate's bf16 autocast); "no": fp32, as the
+        reference runs without autocast (this build's process-wide default is bf16, so "no" must
+        select fp32 explicitly)."""
         if self.mixed_precision == "bf16":
             return F.precision(torch.bfloat16)
         if self.mixed_precision == "fp16":
             raise ValueError("mixed_precision fp16 is not supported by this build (the reference config uses bf16)")
-        return nullcontext()
+        return F.precision(torch.float32)
 
     def _shard(self, dl):
         if self.world == 1 or dl is None or getattr(dl, "batch_sampler", None) is None:

@@ -794,9 +794,28 @@ def harmonic_bwd(x, freqs, append_input, dy, diag_cov=None):
 
 
 # ------------------------------------------------------------------------------------------
-# per-call-site timing for tools/gemm_shapes.py (PROF.detail): every op below is bracketed
-# with HIP events and keyed by op name, tensor shapes and the calling model line.
+# Live timing of the memory-bound ops (bench.py's profiled pass, PROF.enabled): every op below is
+# bracketed with HIP events on the launching stream and keyed "comet_<op>" with its ALGORITHMIC
+# bytes -- every tensor argument read or written once plus every tensor it returns (an output
+# passed in and returned counts once) -- so the bench line carries a TB/s figure per memory-bound
+# op. With PROF.detail (tools/gemm_shapes.py) the key is the op, its tensor shapes and the calling
+# model line instead. Ops called from inside another bracketed op are not bracketed again.
 # ------------------------------------------------------------------------------------------
+_TIMED_DEPTH = [0]
+
+
+def _tensor_bytes(objs, seen):
+    n = 0
+    for a in objs:
+        if isinstance(a, torch.Tensor):
+            if id(a) not in seen:
+                seen.add(id(a))
+                n += a.numel() * a.element_size()
+        elif isinstance(a, (list, tuple)):
+            n += _tensor_bytes(a, seen)
+    return n
+
+
 def _timed(fn):
     import functools
     import os
@@ -804,26 +823,39 @@ def _timed(fn):
 
     @functools.wraps(fn)
     def wrap(*args, **kwargs):
-        if not (PROF.enabled and PROF.detail):
+        if not PROF.enabled or _TIMED_DEPTH[0] > 0:
             return fn(*args, **kwargs)
-        f = sys._getframe(1)
-        while f is not None and f.f_code.co_filename.endswith("ops.py"):
-            f = f.f_back
-        sites = []
-        while f is not None and len(sites) < 2:
-            sites.append(f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}")
-            f = f.f_back
-        site = "<".join(sites) or "?"
-        shapes = ",".join("x".join(map(str, a.shape)) + str(a.dtype)[6:] for a in args if isinstance(a, torch.Tensor))
+        if PROF.detail:
+            f = sys._getframe(1)
+            while f is not None and f.f_code.co_filename.endswith("ops.py"):
+                f = f.f_back
+            sites = []
+            while f is not None and len(sites) < 2:
+                sites.append(f"{os.path.basename(f.f_code.co_filename)}:{f.f_lineno}")
+                f = f.f_back
+            site = "<".join(sites) or "?"
+            shapes = ",".join("x".join(map(str, a.shape)) + str(a.dtype)[6:] for a in args if isinstance(a, torch.Tensor))
+            name = f"{fn.__name__} [{shapes}] @{site}"
+        else:
+            name = "comet_" + fn.__name__
         e0 = PROF.start()
-        out = fn(*args, **kwargs)
-        PROF.stop(e0, f"{fn.__name__} [{shapes}] @{site}")
+        _TIMED_DEPTH[0] += 1
+        try:
+            out = fn(*args, **kwargs)
+        finally:
+            _TIMED_DEPTH[0] -= 1
+        seen = set()
+        nb = _tensor_bytes(args, seen) + _tensor_bytes(kwargs.values(), seen)
+        nb += _tensor_bytes(out if isinstance(out, (list, tuple)) else (out,), seen)
+        PROF.stop(e0, name, 0.0, float(nb))
         return out
     return wrap
 
 
-for _name in ("layernorm", "layernorm_bwd", "cast", "act_bwd", "colsum", "act_bwd_colsum", "instnorm_nhwc", "resize_bilinear",
-              "im2col_nhwc", "act_fwd", "binary", "add_rows", "rowscale", "rowscale_bwd", "sample_bilinear",
-              "corr_sample", "tracker_tokens", "coords_update", "avgpool2_nhwc", "patch_gather", "refine_combine",
-              "track_score", "dino_prep", "pose_encode", "pose_decode", "images_nhwc"):
+for _name in ("layernorm", "layernorm_bwd", "layernorm_bwd_res", "cast", "cast_multi_f32_bf16", "act_bwd", "colsum",
+              "act_bwd_colsum", "instnorm_nhwc", "resize_bilinear", "resize_bilinear_into", "im2col_nhwc", "act_fwd",
+              "binary", "add_rows", "rowscale", "rowscale_bwd", "sample_bilinear", "corr_sample", "tracker_tokens",
+              "coords_update", "avgpool2_nhwc", "patch_gather", "refine_combine", "track_score", "dino_prep",
+              "pose_encode", "pose_decode", "pose_encode3", "pose_decode3", "images_nhwc", "harmonic_fwd",
+              "harmonic_bwd", "sincos_table"):
     globals()[_name] = _timed(globals()[_name])

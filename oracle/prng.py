@@ -113,3 +113,21 @@ def synthetic_batch(seed: int, B: int, T: int, H: int, W: int, N: int):
         "ratio": torch.tensor([0.5], dtype=torch.float64),
     }
     return img, tracks, gt
+
+
+def loop_batches(seed, B=1, T=4, H=128, W=128, N=256, steps=2):
+    """Inputs of the loop golden (tools/gen_golden.py --loop, tests/test_loop_gpu.py): `steps`
+    batches in process_spark_data2's dict layout (train_util.py:637-667; frames and GT from
+    synthetic_batch), an all-true first-frame mask, and the N fixed frame-0 keypoints a SuperPoint
+    stub returns ("kp0"; all inside the mask, so filter_and_pad takes its RNG-free branch when
+    N = min_required = track_num = 256)."""
+    out = []
+    for st in range(steps):
+        img, _, gt = synthetic_batch(seed + 100 * st, B, T, H, W, 16)
+        g = torch.Generator().manual_seed(seed + 100 * st + 7)
+        kp = torch.rand(N, 2, generator=g) * (W - 1)
+        out.append({"images": img, "T": gt["T"].reshape(B, T, 3), "T_uvz": gt["T_uvz"].reshape(B, T, 3),
+                    "R": gt["R"].reshape(B, T, 4), "ratio": gt["ratio"], "fl": gt["focal_length"].reshape(B, T, 2),
+                    "pp": gt["principal_point"].reshape(B, T, 2), "seq_name": [f"seq{st}"],
+                    "first_mask": torch.ones(B, H, W, dtype=torch.bool), "kp0": kp})
+    return out

@@ -5,8 +5,11 @@ mixed-precision forward, backward, clip + AdamW + LR schedule, the eval metrics 
 ckpt_DDDDDD directory of the trained model / optimizer / scheduler round-trips on the device."""
 import os
 
+import numpy as np
 import pytest
 import torch
+
+from conftest import ROOT
 
 import yt_fixture
 
@@ -105,3 +108,81 @@ def test_abl_ours_test_fn_end_to_end(tmp_path):
         v = float(r[k])
         assert v == v, k   # logged and not NaN
     assert float(r["lr"]) == pytest.approx(cfg["train"]["lr"])   # warmup_ratio 0: the base lr at step 0
+
+
+def test_train_or_eval_fn_matches_reference_loop_golden():
+    """The composed training loop against the reference's own train_or_eval_fn run for two steps
+    (tests/golden/comet_golden_loop.npz, tools/gen_golden.py --loop: T=4, 128^2, N=256 fixed
+    keypoint tracks through the loop's keypoint path and filter_and_pad, PRNG weights, fp32):
+    per-step loss and pre-clip gradient norm, the scheduler's learning rates, and the camera
+    predictor's parameter updates after zero_grad -> backward -> clip 1.0 -> AdamW -> scheduler
+    (this build defers the clip scaling into the AdamW kernel). AdamW's first steps move every
+    element by about lr * sign(grad), so the updates are compared by per-parameter norms (2e-2) and
+    element-wise on selected tensors, where elements whose gradient sits at the noise floor may take
+    the other sign (at most 1 % of them)."""
+    from comet_amd.config import instantiate, load_config
+    from comet_amd.loop import CometAccelerator, Stats, TO_PLOT_METRICS, train_or_eval_fn
+    from comet_amd.train import build_optimizer
+    from oracle import prng
+    from oracle.weights import comet_shapes
+    gold = dict(np.load(os.path.join(ROOT, "tests", "golden", "comet_golden_loop.npz"), allow_pickle=False))
+    seed_w, seed_x, B, T, H, W, N, steps = [int(v) for v in gold["loop_cfg"]]
+    cfg = load_config(**{"train.track_num": N, "train.img_size": H, "seqlen": T})
+    cfg["track_by_spsg"] = True
+    cfg["train"]["print_interval"] = 1
+    torch.manual_seed(0)
+    model = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg)
+    model.load_state_dict(prng.make_state_dict(seed_w, comet_shapes()), strict=True)
+    batches = prng.loop_batches(seed_x, B, T, H, W, N, steps)
+    kps = iter([b.pop("kp0").cuda() for b in batches])
+
+    class SP:  # the generator's SuperPoint stub: the fixed keypoints of each batch
+        def extract(self, img):
+            return {"keypoints": next(kps)[None]}
+
+    acc = CometAccelerator(mixed_precision="no")
+    opt, sched = build_optimizer(cfg, model, batches)
+    model, dl, opt, sched = acc.prepare(model, batches, opt, sched)
+    rec = {"loss": [], "norm": [], "lr": []}
+    backward, clip, sstep = acc.backward, acc.clip_grad_norm_, sched.step
+
+    def rec_backward(loss):
+        rec["loss"].append(float(loss.detach()))
+        backward(loss)
+
+    def rec_clip(params, max_norm, optimizer=None):
+        n = clip(params, max_norm, optimizer=optimizer)
+        rec["norm"].append(float(n))
+        return n
+
+    def rec_step(*a, **k):
+        sstep(*a, **k)
+        rec["lr"].append(sched.get_last_lr()[0])
+    acc.backward, acc.clip_grad_norm_, sched.step = rec_backward, rec_clip, rec_step
+    before = {k: p.detach().double().clone() for k, p in model.camera_predictor.named_parameters()}
+    train_or_eval_fn(model, dl, cfg, opt, Stats(TO_PLOT_METRICS), acc, sched, training=True, epoch=0, sp=SP())
+    torch.cuda.synchronize()
+    print("losses", rec["loss"], "ref", gold["loop_loss"], "norms", rec["norm"], "ref", gold["loop_grad_norm"])
+    np.testing.assert_allclose(rec["loss"][0], gold["loop_loss"][0], rtol=2e-4)
+    np.testing.assert_allclose(rec["loss"][1], gold["loop_loss"][1], rtol=1e-3)
+    np.testing.assert_allclose(rec["norm"], gold["loop_grad_norm"], rtol=2e-3)
+    np.testing.assert_allclose(rec["lr"], gold["loop_lr"], rtol=1e-12)
+    named = dict(model.camera_predictor.named_parameters())
+    names = [str(k) for k in gold["loop_names"]]
+    assert sorted(names) == sorted(named)
+    dn = np.array([(named[k].detach().double() - before[k]).norm().item() for k in names])
+    ref = gold["loop_delta_norms"]
+    moved = ref > 0
+    assert ((dn > 0) == moved).all(), [n for n, a, b in zip(names, dn > 0, moved) if a != b][:8]
+    rel = np.abs(dn[moved] - ref[moved]) / ref[moved]
+    print(f"{int(moved.sum())} updated params: max rel diff of the update norms {rel.max():.3e}")
+    assert rel.max() < 2e-2
+    lr = float(gold["loop_lr"][0])
+    for k in gold:
+        if not k.startswith("loop_delta."):
+            continue
+        name = k[len("loop_delta."):]
+        d = (named[name].detach().double() - before[name]).cpu().numpy()
+        off = np.abs(d - gold[k]) > 0.1 * lr
+        print(f"{name}: {off.mean():.2e} of the elements off by > 0.1 lr")
+        assert off.mean() < 1e-2, name

@@ -563,6 +563,134 @@ def gen_metrics(out):
         torch.Tensor.cuda = cuda
 
 
+CFG_LOOP = dict(B=1, T=4, H=128, W=128, N=256, steps=2)
+
+
+def _reference_functions(names):
+    """Top-level functions / classes of train_util.py (whose module imports heavy optional
+    packages) executed from their source in a namespace with math + torch + F."""
+    import ast
+    import math
+    import torch.nn.functional as Fn
+    src = open(os.path.join(H.REF, "comet", "models", "train_util.py")).read()
+    tree = ast.parse(src)
+    nodes = [n for n in tree.body if isinstance(n, (ast.ClassDef, ast.FunctionDef)) and n.name in names]
+    ns = {"math": math, "torch": torch, "F": Fn, "np": np}
+    exec(compile(ast.Module(body=nodes, type_ignores=[]), "train_util.py", "exec"), ns)
+    return ns
+
+
+def gen_loop(out):
+    """SURVEY §8(c) caller counterpart: the reference's own train_or_eval_fn
+    (train_eval_func_new_cp5.py:514-823, training branch) for two steps at the golden size -- keypoint
+    tracks from a SuperPoint stub with fixed keypoints (lightglue is absent; SIFT stubbed empty),
+    process_spark_data2, QuaternionCameras, forward, loss.mean(), the eval-metric block, then
+    zero_grad -> backward (anomaly mode at step 0) -> clip_grad_norm_(1.0) -> AdamW -> scheduler
+    (train_util.build_optimizer), PRNG weights seed 0, fp32. Records the per-step losses, the pre-clip
+    gradient norms, the learning rates and the parameter updates of the camera predictor."""
+    H.install_stubs()
+    q = CFG_LOOP
+    cfg = H.load_cfg()
+    cfg["track_by_spsg"] = True
+    cfg["enable_track"] = True
+    cfg["labor_input_traj"] = False
+    cfg["visual_track"] = False
+    cfg["visual_pose"] = False
+    cfg["train"]["track_num"] = q["N"]
+    cfg["train"]["print_interval"] = 1
+    cfg["train"]["dataset"] = "AMD"
+    torch.manual_seed(0)
+    model = H.build_reference_comet(cfg)
+    P, P_hf = reference_state(model, SEED_W)
+    model.load_state_dict(P_hf, strict=True)
+    M = H.reference_module("train_eval_func_new_cp5")
+    ns = _reference_functions({"process_spark_data2", "WarmupCosineRestarts", "build_optimizer"})
+    M.process_spark_data2 = ns["process_spark_data2"]
+    batches = prng.loop_batches(SEED_X, **{k: q[k] for k in ("B", "T", "H", "W", "N", "steps")})
+    kp_iter = iter([b.pop("kp0") for b in batches])
+
+    class SP:  # lightglue.SuperPoint stand-in: the fixed keypoints of each batch
+        def __init__(self, *a, **k):
+            pass
+
+        def cuda(self):
+            return self
+
+        def eval(self):
+            return self
+
+        def extract(self, img):
+            return {"keypoints": next(kp_iter)[None]}
+
+    class SIFT(SP):
+        def extract(self, img):
+            return {"keypoints": torch.zeros(1, 0, 2)}
+
+    M.SuperPoint, M.SIFT = SP, SIFT
+
+    class Stats:
+        def update(self, *a, **k):
+            pass
+
+        def get_status_string(self, *a, **k):
+            return ""
+
+    rec = {"loss": [], "norm": [], "lr": []}
+
+    class Acc:
+        device = torch.device("cpu")
+
+        def print(self, *a, **k):
+            pass
+
+        def backward(self, loss):
+            rec["loss"].append(float(loss.detach()))
+            loss.backward()
+
+        def clip_grad_norm_(self, params, max_norm):
+            n = torch.nn.utils.clip_grad_norm_(params, max_norm)
+            rec["norm"].append(float(n))
+            return n
+
+    optimizer, sched = ns["build_optimizer"](cfg, model, batches)
+    before = {k: p.detach().clone() for k, p in model.camera_predictor.named_parameters()}
+    orig_step = sched.step
+
+    def step_rec(*a, **k):
+        orig_step(*a, **k)
+        rec["lr"].append(sched.get_last_lr()[0])
+    sched.step = step_rec
+    cuda = torch.Tensor.cuda
+    torch.Tensor.cuda = lambda self, *a, **k: self  # metric.py:337-338 hard-codes .cuda()
+    try:
+        M.train_or_eval_fn(model, batches, cfg, optimizer, Stats(), Acc(), sched, training=True, epoch=0)
+    finally:
+        torch.Tensor.cuda = cuda
+    names = [k for k, p in model.camera_predictor.named_parameters()]
+    delta = {k: (p.detach().double() - before[k].double()) for k, p in model.camera_predictor.named_parameters()}
+    out["loop_cfg"] = np.array([SEED_W, SEED_X, q["B"], q["T"], q["H"], q["W"], q["N"], q["steps"]])
+    out["loop_loss"] = np.array(rec["loss"])
+    out["loop_grad_norm"] = np.array(rec["norm"])
+    out["loop_lr"] = np.array(rec["lr"])
+    out["loop_names"] = np.array(names)
+    out["loop_delta_norms"] = np.array([delta[k].norm().item() for k in names])
+    for k in ["fc_depth.weight", "pose_token", "trunk.3.mlp.fc2.bias", "confidence_attention.0.weight",
+              "traj_encoder.mlp.0.weight", "pose_branch.fc2.weight"]:
+        out["loop_delta." + k] = delta[k].numpy()
+    print("loop golden: losses", rec["loss"], "pre-clip norms", rec["norm"], "lr", rec["lr"],
+          "updated params", int(sum(d.abs().max().item() > 0 for d in delta.values())), "of", len(names))
+
+
+def main_loop():
+    H.require_reference()
+    torch.set_num_threads(8)
+    out = {}
+    gen_loop(out)
+    path = os.path.join(OUT, "comet_golden_loop.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes,", len(out), "arrays")
+
+
 def main_metrics():
     H.require_reference()
     torch.set_num_threads(8)
@@ -828,6 +956,8 @@ def main():
 if __name__ == "__main__":
     if "--v2" in sys.argv:
         main_v2()
+    elif "--loop" in sys.argv:
+        main_loop()
     elif "--ablations" in sys.argv:
         main_ablations()
     elif "--data" in sys.argv:
