@@ -407,6 +407,12 @@ def main():
     elapsed_prof, _ = timed(True)         # same K steps with per-launch HIP events
     comm = None
     if world > 1:
+        # the same K steps without the gradient exchange (backward stays local, bucket hooks idle):
+        # step time with minus without = the all-reduce time the backward does not hide
+        ddp_on = ddp
+        ddp = None
+        elapsed_noar, _ = timed(False)
+        ddp = ddp_on
         # the step's gradient exchange alone: every bucket all-reduced back to back (the in-step
         # all-reduces overlap the backward, so this is an upper bound of what they add)
         nbytes = sum(f.numel() * f.element_size() for f in ddp.flat)
@@ -428,7 +434,9 @@ def main():
                 "bytes_per_step": nbytes, "allreduce_ms_per_step_isolated": round(ms, 3),
                 "algbw_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
                 "busbw_GBps": round(2 * (world - 1) / world * nbytes / (ms * 1e-3) / 1e9, 1),
-                "share_of_step": round(ms / (elapsed / args.steps * 1e3), 4)}
+                "share_of_step": round(ms / (elapsed / args.steps * 1e3), 4),
+                "ms_per_step_without_allreduce": round(elapsed_noar / args.steps * 1e3, 2),
+                "allreduce_exposed_ms_per_step": round((elapsed - elapsed_noar) / args.steps * 1e3, 3)}
     prof_i = PROF.summary(instances=True)
     prof = {}
     for k, v in prof_i.items():

@@ -126,7 +126,9 @@ class GradBucketer:
         self.works.append((bi, dist.all_reduce(self.flat[bi], op=op, group=self.group, async_op=True)))
 
     def _on_grad(self, p):
-        if p in self.arrived:
+        # outside prepare_backward / finish_backward a backward stays local (no bucket, no
+        # collective): bench.py times the step that way to price the exposed all-reduce
+        if not self.in_backward or p in self.arrived:
             return
         self.arrived.add(p)
         self.arrival.append(p)

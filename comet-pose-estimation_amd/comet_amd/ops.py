@@ -797,7 +797,8 @@ def harmonic_bwd(x, freqs, append_input, dy, diag_cov=None):
 # Live timing of the memory-bound ops (bench.py's profiled pass, PROF.enabled): every op below is
 # bracketed with HIP events on the launching stream and keyed "comet_<op>" with its ALGORITHMIC
 # bytes -- every tensor argument read or written once plus every tensor it returns (an output
-# passed in and returned counts once) -- so the bench line carries a TB/s figure per memory-bound
+# passed in and returned counts once; the gather ops count the taps they read, _gather_bytes) --
+# so the bench line carries a TB/s figure per memory-bound
 # op. With PROF.detail (tools/gemm_shapes.py) the key is the op, its tensor shapes and the calling
 # model line instead. Ops called from inside another bracketed op are not bracketed again.
 # ------------------------------------------------------------------------------------------
@@ -814,6 +815,25 @@ def _tensor_bytes(objs, seen):
         elif isinstance(a, (list, tuple)):
             n += _tensor_bytes(a, seen)
     return n
+
+
+def _gather_bytes(name, args, out):
+    """Algorithmic bytes of the gather ops, which read a small part of a large map (the generic
+    rule would count the whole map): the taps actually read + the indices + the output."""
+    nb = lambda t: t.numel() * t.element_size()  # noqa: E731
+    if name == "sample_bilinear":   # 4 bilinear corners per output value
+        fmap, coords = args[0], args[1]
+        return 4 * nb(out) // 4 * fmap.element_size() + nb(coords) + nb(out)
+    if name == "track_score":       # (2r+1)^2 window of each track's patch feature map
+        qfeat, pfeat, fine = args[0], args[1], args[2]
+        r = args[6] if len(args) > 6 else 2
+        C = pfeat.shape[-1]
+        tracks = out[0].numel()
+        return nb(qfeat) + tracks * (2 * r + 1) ** 2 * C * pfeat.element_size() + nb(fine) + nb(out[0]) + nb(out[1])
+    if name == "patch_gather":      # the gathered patches are read once and written once
+        patches = out[0]
+        return 2 * nb(patches) + nb(args[1]) + nb(out[1]) + nb(out[2])
+    return None
 
 
 def _timed(fn):
@@ -844,9 +864,11 @@ def _timed(fn):
             out = fn(*args, **kwargs)
         finally:
             _TIMED_DEPTH[0] -= 1
-        seen = set()
-        nb = _tensor_bytes(args, seen) + _tensor_bytes(kwargs.values(), seen)
-        nb += _tensor_bytes(out if isinstance(out, (list, tuple)) else (out,), seen)
+        nb = _gather_bytes(fn.__name__, args, out)
+        if nb is None:
+            seen = set()
+            nb = _tensor_bytes(args, seen) + _tensor_bytes(kwargs.values(), seen)
+            nb += _tensor_bytes(out if isinstance(out, (list, tuple)) else (out,), seen)
         PROF.stop(e0, name, 0.0, float(nb))
         return out
     return wrap

@@ -199,3 +199,54 @@ def test_prepare_broadcasts_rank0_weights():
     for k in res[0][1]:
         assert np.array_equal(res[0][1][k], res[0][0][k]), k     # rank 0 kept its own
         assert np.array_equal(res[1][1][k], res[0][0][k]), k     # rank 1 got rank 0's
+
+
+def _local_worker(rank, world, port, q, paths):
+    import sys
+    sys.path[:0] = paths
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from comet_amd.ddp import GradBucketer
+        net = _Net()
+        bk = GradBucketer(net.parameters(), bucket_mb=0.004)
+        for step in range(2):  # discovery + one bucketed step
+            net.zero_grad(set_to_none=True)
+            bk.prepare_backward()
+            x, y = _data(rank, step)
+            ((net(x) - y) ** 2).mean().backward()
+            bk.finish_backward()
+        net.zero_grad(set_to_none=True)
+        x, y = _data(rank, 5)
+        ((net(x) - y) ** 2).mean().backward()  # outside prepare / finish: local gradients
+        q.put((rank, {k: p.grad.numpy().copy() for k, p in net.named_parameters() if p.grad is not None},
+               len(bk.launch_log)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_backward_outside_prepare_stays_local():
+    """A backward outside prepare_backward / finish_backward launches no collective and leaves each
+    rank its own gradient (bench.py times the step that way to price the exposed all-reduce)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_local_worker, args=(r, world, port, q, [ROOT, PKG])) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, g, nlog = q.get(timeout=120)
+        got[rank] = g
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in range(world):
+        net = _Net()
+        x, y = _data(rank, 5)
+        ((net(x) - y) ** 2).mean().backward()
+        for k, p in net.named_parameters():
+            if p.grad is not None:
+                torch.testing.assert_close(torch.from_numpy(got[rank][k]), p.grad, rtol=1e-6, atol=1e-7)
