@@ -1420,7 +1420,9 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
         }
         // residual rows are loaded one (i, h) step ahead (a 2-slot register ring), so each step's HBM
         // latency overlaps the previous step's park / reduce / store work instead of being exposed
-        // MI x 2 times (a 3-slot ring measured 4 % slower on the 64 x 384 tiles)
+        // MI x 2 times (a 3-slot ring measured 4 % slower on the 64 x 384 tiles; round 4: every residual
+        // row of a 64 x 384 tile issued at once, and a 4-slot ring on the 128-row tiles, 1-6 % slower,
+        // profiles/r04_rowln)
         constexpr int RDL = 2;
         auto rload = [&](int ih, float (&dst)[NTC][CPL]) {
           const int64_t row = prow0 + (ih >> 1) * 16 + (ih & 1) * 8;

@@ -131,6 +131,196 @@ corr_kernel(PyrTab tab, int levels, int radius, const TT* __restrict__ feats, co
   }
 }
 
+// The same CorrBlock step on the matrix cores, for bf16 maps with C = 128 (the coarse tracker:
+// 512 tracks per frame on a 64 x 64 map). The tracks of one frame read overlapping windows, so
+// the dot products are formed as dense MFMA tiles (16 map pixels x 16 tracks x 32 channels) over
+// the bounding box of 16 tracks' (2r+4)^2 grids, walked in 8 x 2-pixel blocks, and each product
+// inside a track's own grid is kept in an LDS table from which the (2r+1)^2 bilinear samples are
+// taken as in corr_kernel. A workgroup (4 waves x 16 tracks) first ranks the frame's tracks by
+// (8-pixel row band, column) of their level-0 position, so a wave's 16 tracks are neighbours and
+// their box is small; the rank only groups tracks (each product is one MFMA output element, the
+// same whatever the other rows of the tile), and every output row is written by its own track.
+// The f32 track features enter as three bf16 terms (hi + mid + lo == f exactly), so the products
+// are exact as in the f32 kernel and only the summation order differs.
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+template <int C, int RING, int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
+corr_mfma_kernel(PyrTab tab, int levels, int radius, const float* __restrict__ feats,
+                 const float* __restrict__ coords, float* __restrict__ out, int64_t ldo, int64_t col0, int N, int S,
+                 int frames, float inv_sqrt_c, int sort) {
+  constexpr int KS = C / 32;  // 32-channel k-steps
+  extern __shared__ __attribute__((aligned(16))) float csm[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int li = lane & 15, hg = lane >> 4;
+  const int gs = 2 * radius + 4, g2 = gs * gs, win = 2 * radius + 1, nw = win * win;
+  const int tiles = (N + 63) / 64;
+  // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin, so frame f's tiles all get
+  // blockIdx = f (mod 8) and share one XCD's L2 (the frame's pyramid is read by all of them)
+  const int xcd = (int)(blockIdx.x & 7), q = (int)(blockIdx.x >> 3);
+  const int f = (q / tiles) * 8 + xcd, r0 = (q % tiles) * 64;
+  if (f >= frames) return;
+  const int b = f / S, s = f % S;
+  float* dt = csm + wid * 16 * g2;  // this wave's [16 tracks][gs * gs] dots
+  int* slot = reinterpret_cast<int*>(csm + 4 * 16 * g2);
+  unsigned* keys = reinterpret_cast<unsigned*>(slot + 64);
+  if (sort) {
+    // key = band (10 bits) | column (11 bits) | track (11 bits, N <= 2048): distinct, so a track's
+    // rank is the number of smaller keys
+    const int np = (N + 3) & ~3;
+    for (int n = tid; n < np; n += 256) {
+      unsigned key = 0xffffffffu;
+      if (n < N) {
+        const float* c = coords + (((int64_t)b * N + n) * S + s) * 2;
+        const float band = fminf(fmaxf(floorf(c[1] * 0.125f), -8.f), 1015.f) + 8.f;
+        const float col = fminf(fmaxf(floorf(c[0]), -64.f), 1983.f) + 64.f;
+        key = ((unsigned)band << 22) | ((unsigned)col << 11) | (unsigned)n;
+      }
+      keys[n] = key;
+    }
+    __syncthreads();
+    for (int n0 = 0; n0 < N; n0 += 512) {
+      const int na = n0 + tid, nb = n0 + 256 + tid;
+      const unsigned ka = na < N ? keys[na] : 0u, kb = nb < N ? keys[nb] : 0u;
+      int ra = 0, rb = 0;
+      for (int m = 0; m < np; m += 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(keys + m);
+        ra += (v.x < ka) + (v.y < ka) + (v.z < ka) + (v.w < ka);
+        rb += (v.x < kb) + (v.y < kb) + (v.z < kb) + (v.w < kb);
+      }
+      if (na < N && ra >= r0 && ra < r0 + 64) slot[ra - r0] = na;
+      if (nb < N && rb >= r0 && rb < r0 + 64) slot[rb - r0] = nb;
+    }
+  } else if (tid < 64) {
+    slot[tid] = r0 + tid;
+  }
+  __syncthreads();
+  const bool act = r0 + wid * 16 + li < N;
+  const int n = act ? slot[wid * 16 + li] : 0;
+  const int64_t t = ((int64_t)b * N + n) * S + s;
+  // track features as three bf16 terms, B operand layout: track li, channels 32 ks + 8 hg ..
+  bf16x8 tf[3][KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    f32x8 v{};
+    if (act) {
+      const float4* p = reinterpret_cast<const float4*>(feats + t * C + 32 * ks + 8 * hg);
+      const float4 x0 = p[0], x1 = p[1];
+      v = f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      tf[u][ks] = __builtin_convertvector(v, bf16x8);
+      v -= __builtin_convertvector(tf[u][ks], f32x8);
+    }
+  }
+  const float cx = act ? coords[t * 2] : 0.f, cy = act ? coords[t * 2 + 1] : 0.f;
+  for (int l = 0; l < levels; ++l) {
+    const int H = tab.h[l], W = tab.w[l];
+    const __bf16* fm = reinterpret_cast<const __bf16*>(tab.p[l]) + (int64_t)f * H * W * C;
+    const float scl = 1.f / (float)(1 << l);
+    const float xl = cx * scl, yl = cy * scl;
+    // grid origin, clamped so that NaN / huge coordinates give an empty intersection with the map
+    const int gx0 = (int)fminf(fmaxf(floorf(xl), -65536.f), 65536.f) - radius - 1;
+    const int gy0 = (int)fminf(fmaxf(floorf(yl), -65536.f), 65536.f) - radius - 1;
+    int bx0 = act ? gx0 : 1 << 30, by0 = act ? gy0 : 1 << 30;
+    int bx1 = act ? gx0 + gs - 1 : -(1 << 30), by1 = act ? gy0 + gs - 1 : -(1 << 30);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      bx0 = min(bx0, __shfl_xor(bx0, o, 64));
+      by0 = min(by0, __shfl_xor(by0, o, 64));
+      bx1 = max(bx1, __shfl_xor(bx1, o, 64));
+      by1 = max(by1, __shfl_xor(by1, o, 64));
+    }
+    // the box is wave-uniform: say so, so that the block loop and its index math run on the SALU
+    bx0 = __builtin_amdgcn_readfirstlane(max(bx0, 0));
+    by0 = __builtin_amdgcn_readfirstlane(max(by0, 0));
+    bx1 = __builtin_amdgcn_readfirstlane(min(bx1, W - 1));
+    by1 = __builtin_amdgcn_readfirstlane(min(by1, H - 1));
+    // 8 x 2-pixel blocks over the box: nbx across, nby down (none when the box misses the map)
+    const int nbx = bx1 >= bx0 ? (bx1 - bx0 + 8) >> 3 : 0, nby = by1 >= by0 ? (by1 - by0 + 2) >> 1 : 0;
+    const int nblk = nbx * nby;
+    // zero the table (pixels outside the map keep a zero dot product)
+    for (int i = lane; i < 4 * g2; i += 64) reinterpret_cast<float4*>(dt)[i] = float4{0.f, 0.f, 0.f, 0.f};
+    // A operand: pixel li of the block = (bx0 + 8 cb + (li & 7), by0 + 2 rb + (li >> 3)); a pixel
+    // past the box's edge loads the edge pixel instead (its output row is never stored), so the
+    // loads are unconditional
+    auto aload = [&](int blk, bf16x8 (&a)[KS]) {
+      const int rb = blk / nbx, cb = blk - rb * nbx;
+      const int px = min(bx0 + 8 * cb + (li & 7), bx1), py = min(by0 + 2 * rb + (li >> 3), by1);
+      const __bf16* src = fm + ((int64_t)py * W + px) * C + 8 * hg;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) a[ks] = *reinterpret_cast<const bf16x8*>(src + 32 * ks);
+    };
+    // this lane's outputs: pixels 4 hg + e of the block = columns 4 (hg & 1) + e of row hg >> 1
+    const int cxe = bx0 + 4 * (hg & 1), ry = by0 + (hg >> 1);
+    auto blkstep = [&](int blk, const bf16x8 (&ac)[KS]) {
+      f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int u = 0; u < 3; ++u) d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ac[ks], tf[u][ks], d, 0, 0, 0);
+      const int rb = blk / nbx, cb = blk - rb * nbx;
+      const int px = cxe + 8 * cb, py = ry + 2 * rb;
+      const int gx = px - gx0, gy = py - gy0;
+      if (act && py <= by1 && (unsigned)gy < (unsigned)gs) {
+        float* trow = dt + li * g2 + gy * gs + gx;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (px + e <= bx1 && (unsigned)(gx + e) < (unsigned)gs) trow[e] = d[e] * inv_sqrt_c;
+      }
+    };
+    // a ring of RING register buffers with static indices (a runtime index into a register array
+    // becomes indexed-register moves): RING - 1 blocks of pixels load while a block's MFMAs run. The
+    // prefetch is unconditional (past the last block it reloads the last one) so that the wait
+    // before the MFMAs counts exactly the older block's loads
+    bf16x8 ring[RING][KS];
+    if (nblk > 0) {
+#pragma unroll
+      for (int u = 0; u < RING - 1; ++u) aload(min(u, nblk - 1), ring[u]);
+    }
+    for (int blk0 = 0; blk0 < nblk; blk0 += RING) {
+#pragma unroll
+      for (int u = 0; u < RING; ++u) {
+        const int blk = blk0 + u;
+        if (blk < nblk) {
+          aload(min(blk + RING - 1, nblk - 1), ring[(u + RING - 1) % RING]);
+          blkstep(blk, ring[u]);
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    // (2r+1)^2 bilinear samples per track from the table, the arithmetic of corr_kernel: one task per
+    // (track, window column i) computes the x terms once and walks the window rows j
+    for (int k0 = 0; k0 < 16 * win; k0 += 64) {  // uniform trip count: every lane joins the shuffles
+      const int k = k0 + lane;
+      const int ti = min(k / win, 15), i = k - ti * win;
+      const float tx = __shfl(xl, ti, 64), ty = __shfl(yl, ti, 64);
+      const int ox = __shfl(gx0, ti, 64), oy = __shfl(gy0, ti, 64), tn = __shfl(n, ti, 64);
+      if (k >= 16 * win || r0 + wid * 16 + ti >= N) continue;
+      float* orow = out + (((int64_t)b * N + tn) * S + s) * ldo + col0 + l * nw + i * win;
+      const float ix = src_index(tx + (float)(i - radius), W, false);
+      const int x0 = (int)floorf(ix);
+      const int gxa = x0 - ox;
+      const bool xa = (unsigned)gxa < (unsigned)gs, xb = (unsigned)(gxa + 1) < (unsigned)gs;
+      const float* col = dt + ti * g2 + gxa;
+      for (int j = 0; j < win; ++j) {
+        const float iy = src_index(ty + (float)(j - radius), H, false);
+        const int y0 = (int)floorf(iy);
+        const float wnw = ((float)(x0 + 1) - ix) * ((float)(y0 + 1) - iy), wne = (ix - (float)x0) * ((float)(y0 + 1) - iy);
+        const float wsw = ((float)(x0 + 1) - ix) * (iy - (float)y0), wse = (ix - (float)x0) * (iy - (float)y0);
+        const int gya = y0 - oy;
+        const bool ya = (unsigned)gya < (unsigned)gs, yb = (unsigned)(gya + 1) < (unsigned)gs;
+        const float* c0 = col + gya * gs;
+        const float d00 = xa && ya ? c0[0] : 0.f, d10 = xb && ya ? c0[1] : 0.f;
+        const float d01 = xa && yb ? c0[gs] : 0.f, d11 = xb && yb ? c0[gs + 1] : 0.f;
+        orow[j] = d00 * wnw + d10 * wne + d01 * wsw + d11 * wse;
+      }
+    }
+    asm volatile("" ::: "memory");
+  }
+}
+
 template <typename TO>
 __global__ void tokens_kernel(const float* __restrict__ coords, const float* __restrict__ feats, int latent,
                               const float* __restrict__ corr, int64_t ldcorr, int corrdim,
@@ -571,6 +761,23 @@ extern "C" int comet_corr_sample(int dtype_fmap, int dtype_feat, const void* con
   }
   hipStream_t s = as_stream(stream);
   const float isc = 1.f / sqrtf((float)C);
+  const bool valu = std::getenv("COMET_CORR_VALU") != nullptr;  // the VALU kernel for every shape (A/B, tests)
+  if (dtype_fmap == COMET_BF16 && C == 128 && N >= 16 && !valu) {
+    // matrix-core path (corr_mfma_kernel): 4 waves x 16 tracks per workgroup
+    const int gs = 2 * radius + 4, sort = N <= 2048;
+    const size_t lds = (size_t)4 * 16 * gs * gs * 4 + 64 * 4 + (sort ? (size_t)((N + 3) & ~3) * 4 : 0);
+    const int64_t frames = B * S, grid = (frames + 7) / 8 * 8 * ((N + 63) / 64);
+    COMET_CHECK_ARG(grid < (1ll << 31) && N < (1ll << 30), "comet_corr_sample: too many tracks");
+    const char* rs = std::getenv("COMET_CORR_RING");
+    const int ring = rs ? std::atoi(rs) : 2;
+    const bool occ4 = std::getenv("COMET_CORR_OCC4") != nullptr;
+#define CM(R, O) hipLaunchKernelGGL((corr_mfma_kernel<128, R, O>), dim3((unsigned)grid), dim3(256), lds, s, tab, levels, \
+                                    radius, (const float*)feats, coords, out, ldo, col0, (int)N, S, (int)frames, isc, sort)
+    if (occ4) CM(2, 4); else if (ring >= 4) CM(4, 1); else if (ring == 3) CM(3, 1); else CM(2, 1);
+#undef CM
+    COMET_CHECK_LAUNCH("comet_corr_sample");
+    return COMET_OK;
+  }
 #define CK(TF, CC) hipLaunchKernelGGL((corr_kernel<TF, float, CC>), dim3((unsigned)T), dim3(256), 0, s, tab, levels, radius, (const float*)feats, coords, out, ldo, col0, N, S, isc)
   if (dtype_fmap == COMET_F32) { if (C == 128) CK(float, 128); else CK(float, 32); }
   else { if (C == 128) CK(__bf16, 128); else CK(__bf16, 32); }

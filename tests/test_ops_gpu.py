@@ -798,6 +798,62 @@ def test_corr_sample_vs_f64(C, radius, dtype):
     assert (out[:, :2] == 7.0).all() and (out[:, 2 + levels * win * win:] == 7.0).all()
 
 
+@pytest.mark.parametrize("layout", ["uniform", "clustered", "outside"])
+def test_corr_sample_mfma_vs_f64(layout):
+    """The matrix-core CorrBlock path (bf16 maps, C = 128, >= 16 tracks per frame: the coarse
+    tracker's case) vs the f64 restatement: N = 200 tracks per frame (not a multiple of the 16-track
+    wave groups or the 64-track workgroups), 4 levels; tracks spread over the map, all in one spot
+    (every wave's box the same), or partly far outside the map."""
+    ops = _ops()
+    B, N, S, levels, radius, C, H0 = 1, 200, 2, 4, 4, 128, 40
+    pyr = [_rand(B * S, H0 >> l, H0 >> l, C, seed=240 + l).to(torch.bfloat16).to(DEV) for l in range(levels)]
+    rows = B * N * S
+    feats = _rand(rows, C, seed=250)
+    g = torch.Generator().manual_seed(251)
+    if layout == "uniform":
+        coords = torch.rand(rows, 2, generator=g) * (H0 + 8) - 4
+    elif layout == "clustered":
+        coords = 17.3 + torch.rand(rows, 2, generator=g) * 0.5
+    else:
+        coords = torch.rand(rows, 2, generator=g) * (H0 + 8) - 4
+        coords[::3] = coords[::3] * 40 - 800
+    win = 2 * radius + 1
+    out = torch.full((rows, levels * win * win + 3), 7.0, device=DEV)
+    ops.corr_sample(pyr, radius, feats.to(DEV), coords.to(DEV), out, 1, B, N, S)
+    ref = _corr_ref(pyr, radius, feats, coords, B, N, S)
+    _close(out[:, 1:1 + levels * win * win], ref, 1e-4, 1e-4, f"corr mfma {layout}")
+    assert (out[:, :1] == 7.0).all() and (out[:, 1 + levels * win * win:] == 7.0).all()
+
+
+def test_corr_sample_mfma_matches_valu_headline(monkeypatch):
+    """At the coarse tracker's headline shape per frame (N = 512 tracks, 64 x 64 x 128 bf16 maps,
+    4 levels, radius 4), the matrix-core path equals the VALU kernel (COMET_CORR_VALU=1) up to f32
+    summation order; tracks with NaN coordinates leave the other tracks' rows untouched."""
+    ops = _ops()
+    B, N, S, levels, radius, C, H0 = 2, 512, 3, 4, 4, 128, 64
+    pyr = [(_rand(B * S, H0 >> l, H0 >> l, C, seed=260 + l) * 2).to(torch.bfloat16).to(DEV) for l in range(levels)]
+    rows = B * N * S
+    feats = _rand(rows, C, seed=270).to(DEV)
+    coords = (torch.rand(rows, 2, generator=torch.Generator().manual_seed(271)) * 70 - 3).to(DEV)
+    coords[5] = float("nan")
+    win = 2 * radius + 1
+    outs = []
+    for valu in (False, True):
+        if valu:
+            monkeypatch.setenv("COMET_CORR_VALU", "1")
+        o = torch.empty(rows, levels * win * win, device=DEV)
+        ops.corr_sample(pyr, radius, feats, coords, o, 0, B, N, S)
+        outs.append(o)
+    ok = torch.ones(rows, dtype=torch.bool, device=DEV)
+    ok[5] = False
+    a, v = outs[0][ok], outs[1][ok]
+    assert torch.isfinite(a).all()
+    # both sum 128 exact products in f32, in different orders: the difference is f32 rounding of
+    # sums whose terms reach ~|v|max, so it is bounded against the output scale, not per element
+    err = ((a - v).abs().max() / v.abs().max()).item()
+    assert err < 2e-6, err
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_resize_into_channel_slices(dtype):
     """BasicEncoder concat (blocks.py:102-107): four maps resized straight into their channel
