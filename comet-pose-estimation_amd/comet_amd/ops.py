@@ -830,6 +830,15 @@ def _gather_bytes(name, args, out):
         C = pfeat.shape[-1]
         tracks = out[0].numel()
         return nb(qfeat) + tracks * (2 * r + 1) ** 2 * C * pfeat.element_size() + nb(fine) + nb(out[0]) + nb(out[1])
+    if name == "corr_sample":       # each track's (2r+4)^2 pixel grid per level, at most every pixel once
+        pyramid, radius, feats, coords, o = args[0], args[1], args[2], args[3], args[4]
+        gs = 2 * radius + 4
+        tracks = coords.shape[0]
+        n = nb(feats) + nb(coords) + o.shape[0] * len(pyramid) * (2 * radius + 1) ** 2 * o.element_size()
+        for lv in pyramid:
+            fr, H, W, C = lv.shape
+            n += min(tracks * min(gs, H) * min(gs, W), fr * H * W) * C * lv.element_size()
+        return n
     if name == "patch_gather":      # the gathered patches are read once and written once
         patches = out[0]
         return 2 * nb(patches) + nb(args[1]) + nb(out[1]) + nb(out[2])

@@ -93,3 +93,27 @@ def test_world_size_must_match_gpus():
     r = _run(["--gpus", "4", "--launcher-check"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_gather_ops_count_the_bytes_they_read():
+    """The bench line's TB/s for the gather ops uses the bytes the kernels read, not the whole map:
+    CorrBlock sampling counts each track's (2r+4)^2 grid per level, at most every pixel of a frame
+    once (the coarse 64 x 64 maps are covered by 512 tracks; the fine 31 x 31 patch maps are read only
+    in their 10 x 10 windows)."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "comet-pose-estimation_amd"))
+    from comet_amd import ops
+    B, N, S, C, r = 2, 512, 3, 128, 4
+    pyr = [torch.zeros(B * S, 64 >> l, 64 >> l, C, dtype=torch.bfloat16) for l in range(4)]
+    rows = B * N * S
+    feats, coords = torch.zeros(rows, C), torch.zeros(rows, 2)
+    out = torch.zeros(rows, 4 * 81)
+    n = ops._gather_bytes("corr_sample", (pyr, r, feats, coords, out, 0, B, N, S), None)
+    maps = sum(p.numel() * 2 for p in pyr)  # every pixel once
+    assert n == maps + feats.numel() * 4 + coords.numel() * 4 + out.numel() * 4
+    fine = [torch.zeros(rows, 31 >> l, 31 >> l, 32, dtype=torch.bfloat16) for l in range(3)]
+    o2 = torch.zeros(rows, 3 * 49)
+    n2 = ops._gather_bytes("corr_sample", (fine, 3, torch.zeros(rows, 32), coords, o2, 0, rows, 1, 1), None)
+    win = rows * (100 + 100 + 49) * 32 * 2
+    assert n2 == win + rows * 32 * 4 + coords.numel() * 4 + o2.numel() * 4
+    assert n2 < sum(p.numel() * 2 for p in fine) / 2

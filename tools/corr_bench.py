@@ -55,4 +55,4 @@ def run(C, r, B, N, S, H0, levels, reps=10, clustered=False):
 
 run(128, 4, 8, 512, 16, 64, 4)
 run(128, 4, 8, 512, 16, 64, 4, clustered=True)
-run(32, 3, 8 * 512, 1, 15, 31, 1)
+run(32, 3, 8 * 512, 1, 15, 31, 3)
