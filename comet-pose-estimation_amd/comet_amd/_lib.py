@@ -99,6 +99,8 @@ SIGNATURES = {
     "comet_gemm_plan": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_int32)]),
     "comet_gemm_rowln_ok": (_INT, [ctypes.POINTER(GemmArgs)]),
     "comet_gemm_rowln": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(RowLNArgs), c_vp]),
+    "comet_gemm_dact_ok": (_INT, [ctypes.POINTER(GemmArgs), _INT, c_vp, c_i64]),
+    "comet_gemm_dact": (_INT, [ctypes.POINTER(GemmArgs), _INT, c_vp, c_i64, c_vp, c_vp]),
     "comet_conv2d_nhwc": (_INT, [ctypes.POINTER(ConvArgs), c_vp]),
     "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
                                    c_i64, _F, _INT, c_vp]),

@@ -237,6 +237,78 @@ def linear(x, w, b=None, act=L.ACT_NONE, resid=None, beta=1.0, out_dtype=None):
     return ops.linear(xc, wc, bias=b, act=act, resid=resid, beta=beta, out_dtype=out_dtype)
 
 
+class _Mlp(torch.autograd.Function):
+    """fc1 -> GELU -> fc2 (+ residual) as one node (timm Mlp of the camera head's blocks,
+    modules.py:18-40), so that its backward can hand fc1's GELU backward and bias gradient to the
+    epilogue of fc2's input-gradient GEMM (comet_gemm_dact): the [M, hidden] gradient is written
+    once in bf16 instead of written (dH), read with the pre-activation and written again
+    (comet_act_bwd_colsum). The forward and the four other GEMMs of the backward are _Linear's."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, resid, out_dtype):
+        wc1, wc2 = wcast(w1, torch.bfloat16), wcast(w2, torch.bfloat16)
+        xc = x if x.dtype == torch.bfloat16 else ops.cast(x, torch.bfloat16)
+        shp = x.shape
+        x2 = xc.reshape(-1, shp[-1])
+        Hd, N = w1.shape[0], w2.shape[0]
+        aux = torch.empty(x2.shape[0], Hd, device=x.device, dtype=torch.bfloat16)
+        h = ops.linear(x2, wc1, bias=b1, act=L.ACT_GELU, out_dtype=torch.bfloat16, aux=aux)
+        y = ops.linear(h, wc2, bias=b2, resid=(resid.reshape(-1, N) if resid is not None else None),
+                       out_dtype=out_dtype)
+        ctx.save_for_backward(x2, h, aux, w1, w2)
+        ctx.xdtype, ctx.shape = x.dtype, shp
+        ctx.has_b1, ctx.has_b2, ctx.has_r = b1 is not None, b2 is not None, resid is not None
+        return y.reshape(*shp[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, aux, w1, w2 = ctx.saved_tensors
+        N = w2.shape[0]
+        dy2 = dy.reshape(-1, N)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        wc1, wc2 = wcast(w1, torch.bfloat16), wcast(w2, torch.bfloat16)
+        ni = ctx.needs_input_grad
+        # fc2: the bf16 operand of its two GEMMs and its bias gradient in one pass, then dW2 (its dX
+        # is the fused GEMM below)
+        db2 = torch.empty(N, device=dy.device, dtype=torch.float32) if ctx.has_b2 and ni[4] else None
+        if dy2.dtype == torch.bfloat16:
+            dpre2 = dy2
+            if db2 is not None:
+                ops.act_bwd_colsum(L.ACT_NONE, None, dy2, dbias=db2, want_out=False)
+        else:
+            dpre2 = ops.act_bwd_colsum(L.ACT_NONE, None, dy2, out_dtype=torch.bfloat16, dbias=db2)
+        _, dw2, _ = _linear_bwd(h, wc2, dpre2, L.ACT_NONE, None, False, ni[3], False, torch.bfloat16)
+        db1 = torch.empty(w1.shape[0], device=dy.device, dtype=torch.float32) if ctx.has_b1 and ni[2] else None
+        if ops.linear_dact_ok(dpre2, wc2, aux, L.ACT_GELU):
+            dpre1 = ops.linear_dact(dpre2, wc2, aux, L.ACT_GELU, dbias=db1)
+        else:
+            dh = torch.empty(h.shape, device=dy.device, dtype=torch.bfloat16)
+            ops.gemm_raw(dpre2, wc2, dh, m=dh.shape[0], n=dh.shape[1], k=N, layout_a=0, lda=dpre2.stride(0),
+                         layout_b=1, ldb=wc2.stride(0), ldc=dh.shape[1], compute=torch.bfloat16)
+            dpre1 = ops.act_bwd_colsum(L.ACT_GELU, aux, dh, out_dtype=torch.bfloat16, dbias=db1)
+        # fc1: dpre1 is already the activation's input gradient and db1 its column sum
+        dx, dw1, _ = _linear_bwd(x2, wc1, dpre1, L.ACT_NONE, None, ni[0], ni[1], False, ctx.xdtype)
+        if dx is not None:
+            dx = dx.reshape(ctx.shape)
+            if dx.dtype != ctx.xdtype:
+                dx = ops.cast(dx, ctx.xdtype)
+        dres = dy if ctx.has_r and ni[5] else None
+        return dx, dw1, db1, dw2, db2, dres, None
+
+
+def mlp(x, w1, b1, w2, b2, resid=None, out_dtype=torch.float32):
+    """fc2(GELU(fc1(x))) (+ resid). In bf16 compute with gradients one autograd node (_Mlp); the
+    fused backward can be switched off with COMET_NO_MLP_FUSE=1 (A/B)."""
+    if compute_dtype() == torch.bfloat16 and _needs_grad(x, w1, b1, w2, b2, resid) and not _MLP_UNFUSED:
+        return _Mlp.apply(x, w1, b1, w2, b2, resid, out_dtype)
+    h = linear(x, w1, b1, act=L.ACT_GELU)
+    return linear(h, w2, b2, resid=resid, out_dtype=out_dtype)
+
+
+_MLP_UNFUSED = os.environ.get("COMET_NO_MLP_FUSE") is not None
+
+
 # ------------------------------------------------------------------------------------------
 # layernorm (f32 in / f32 out)
 # ------------------------------------------------------------------------------------------

@@ -30,8 +30,7 @@ class Mlp(nn.Module):
         self.drop2 = nn.Dropout(drop)
 
     def forward(self, x, resid=None, out_dtype=torch.float32):
-        h = F.linear(x, self.fc1.weight, self.fc1.bias, act=L.ACT_GELU)
-        return F.linear(h, self.fc2.weight, self.fc2.bias, resid=resid, out_dtype=out_dtype)
+        return F.mlp(x, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias, resid=resid, out_dtype=out_dtype)
 
 
 def _mha_holder(C, heads):

@@ -195,6 +195,51 @@ def linear_rowln_ok(x, w, resid):
     return bool(L.load().comet_gemm_rowln_ok(ctypes.byref(g)))
 
 
+def _dact_args(dy2, wc, out):
+    M, N2 = dy2.shape
+    K2 = wc.shape[1]
+    g = L.GemmArgs()
+    g.dtype_ab, g.dtype_c, g.layout_a, g.layout_b = L.BF16, L.BF16, 0, 1
+    g.m, g.n, g.k = M, K2, N2
+    g.batch[0] = g.batch[1] = 1
+    g.a, g.lda = dy2.data_ptr(), dy2.stride(0)
+    g.b, g.ldb = wc.data_ptr(), wc.stride(0)
+    g.c, g.ldc = out.data_ptr(), out.stride(0)
+    g.alpha, g.beta, g.act = 1.0, 1.0, L.ACT_NONE
+    return g
+
+
+def linear_dact_ok(dy2, wc, pre, act):
+    """True when comet_gemm_dact takes the input gradient of y = Linear(h) fused with the backward
+    of h = act(pre) (bf16 dY [M, N2] and weight [N2, K2], pre bf16 [M, K2]; include/comet_hip.h)."""
+    if dy2.dtype != torch.bfloat16 or wc.dtype != torch.bfloat16 or pre is None or pre.dtype != torch.bfloat16:
+        return False
+    if dy2.dim() != 2 or pre.dim() != 2 or dy2.stride(-1) != 1 or wc.stride(-1) != 1 or pre.stride(-1) != 1:
+        return False
+    if pre.shape != (dy2.shape[0], wc.shape[1]) or dy2.shape[1] != wc.shape[0]:
+        return False
+    g = _dact_args(dy2, wc, pre)  # alignment of the output is that of a fresh tensor
+    return bool(L.load().comet_gemm_dact_ok(ctypes.byref(g), act, pre.data_ptr(), pre.stride(0)))
+
+
+def linear_dact(dy2, wc, pre, act, dbias=None):
+    """dPre = act'(pre) * (dY @ W) in bf16 and dbias = its column sums, in one kernel
+    (comet_gemm_dact): the hidden gradient of an MLP, fc2's dX fused with fc1's activation
+    backward. dY [M, N2] bf16, W [N2, K2] (fc2.weight in the compute dtype), pre [M, K2] bf16."""
+    _req_cuda(dy2, wc, pre, dbias)
+    M, K2 = dy2.shape[0], wc.shape[1]
+    out = torch.empty(M, K2, device=dy2.device, dtype=torch.bfloat16)
+    g = _dact_args(dy2, wc, out)
+    e0 = PROF.start()
+    L.check(L.load().comet_gemm_dact(ctypes.byref(g), act, pre.data_ptr(), pre.stride(0), _p(dbias), stream()),
+            "comet_gemm_dact")
+    if e0 is not None:
+        N2 = dy2.shape[1]
+        name = f"gemm_dact M{M} N{K2} K{N2}" if PROF.detail else "comet_gemm_dact"
+        PROF.stop(e0, name, 2.0 * M * K2 * N2, float(2 * M * N2 + 2 * N2 * K2 + 2 * M * K2 * 2))
+    return out
+
+
 def linear_rowln(x, w, bias, resid, *, raw=True, y16_eps=None, z=None):
     """v = x @ w^T + bias + resid (f32) with the row LayerNorms its consumers need written by the
     same kernel (comet_gemm_rowln). Returns (c, y16, z16):

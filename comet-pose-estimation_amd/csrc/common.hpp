@@ -189,6 +189,21 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);
   return cdf + x * pdf;
 }
+// d/dx of gelu_erf with the same branch-free erf (A&S 7.1.26, |err| <= 1.5e-7) and one exp shared
+// by the cdf and pdf terms (libm erff branches on |x| < 1 and made the GELU backward VALU-bound);
+// shared by comet_act_bwd_colsum and the GEMM epilogue that applies a GELU backward (gemm.hip)
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __expf(-z * z);  // = exp(-x^2 / 2)
+  const float erf_v = copysignf(1.0f - p * t * e, x);
+  return 0.5f * (1.0f + erf_v) + x * (0.39894228040143267794f * e);
+}
+
 __device__ __forceinline__ float apply_act(int act, float v) {
   switch (act) {
     case COMET_ACT_GELU: return gelu_erf(v);

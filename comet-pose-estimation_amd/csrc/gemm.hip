@@ -43,6 +43,9 @@ struct Epi {
   int wide = 0;  // persistent kernel: 16-B bf16 stores (C 16-B aligned, ldc % 8 == 0; host-checked)
   int prio = 0;  // persistent kernel: s_setprio 1 for waves 4-7 (COMET_GEMM_PRIO=1, measurement)
   int bpark = 0;  // persistent kernel: bf16-park epilogue (COMET_GEMM_NO_BPARK=1: the direct / f32-park paths)
+  // 256-row kernel, DACT instances (comet_gemm_dact): C = act'(pre) * acc with pre [M, N] bf16 at
+  // row pitch ldg, and dcol[n] += sum over rows of the stored (rounded) values
+  const __bf16* gpre = nullptr; int64_t ldg = 0; float* dcol = nullptr;
 };
 
 // Split-K partials: ws[((z * nb) + bz) * M * N + row * N + col], f32.
@@ -767,7 +770,7 @@ __device__ __forceinline__ bf16x8 frag_t(const __bf16* __restrict__ img, int rba
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-template <typename TC, int BN, int LA, int LB, bool SPLIT, int VAR = 0>
+template <typename TC, int BN, int LA, int LB, bool SPLIT, int VAR = 0, bool DACT = false>
 __global__ void __launch_bounds__(NT, 1)
 gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                 TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, Epi epi,
@@ -889,9 +892,12 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
   const int rq = g * 4;
   const int cg = lane & 7, rb = lane >> 3;
   const int64_t col0 = n0 + wc * 64 + cg * 8;
-  float bc[8];
+  float bc[8], cs[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bc[e] = (epi.bias && epi.bias_mode == 1 && col0 + e < N) ? epi.bias[col0 + e] : 0.f;
+  for (int e = 0; e < 8; ++e) {
+    bc[e] = (epi.bias && epi.bias_mode == 1 && col0 + e < N) ? epi.bias[col0 + e] : 0.f;
+    cs[e] = 0.f;
+  }
 #pragma unroll
   for (int h = 0; h < MI / 4; ++h) {
     if (h) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -922,6 +928,18 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
         }
         continue;
       }
+      if constexpr (DACT) {  // backward of an activation: act'(pre) * dH, rounded, column sums
+        float pr[8];
+        load8(epi.gpre + row * epi.ldg + col0, pr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float gq = to_f32(from_f32<TC>(epi.alpha * v[e] * gelu_grad_fast(pr[e])));
+          v[e] = gq;
+          cs[e] += gq;
+        }
+        store8(C + row * ldc + col0, v);
+        continue;
+      }
       const float br = (epi.bias && epi.bias_mode == 2) ? epi.bias[row] : 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = epi.alpha * v[e] + bc[e] + br;
@@ -946,6 +964,24 @@ gemm_big_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restr
           if (R) o += epi.beta * to_f32(R[row * epi.ldr + col]);
           C[row * ldc + col] = from_f32<TC>(o);
         }
+      }
+    }
+  }
+  if constexpr (DACT) {
+    // the 8 row lanes of each column group (lanes cg + 8 rb) meet by shuffles; one atomic per column
+    // per wave (the act_bwd_colsum kernel sums its row blocks the same way)
+    if (epi.dcol != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = cs[e];
+        x += __shfl_xor(x, 8, 64);
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
+        cs[e] = x;
+      }
+      if (rb == 0 && col0 < N) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) atomicAdd(epi.dcol + col0 + e, cs[e]);
       }
     }
   }
@@ -1027,7 +1063,11 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   constexpr int NI = WCOLS / 16;    // column fragments per wave
   constexpr int ASTAGE = TBM * BK;  // bf16 elements of the A image of one k-tile
   constexpr int BUF = (TBM + TBN) * BK;  // A + B images of one k-tile (64 KiB)
-  constexpr int PA = TBM / 8 / NW, PB = TBN / 8 / NW;  // LDS-DMA pieces per wave and k-tile
+  // LDS-DMA pieces (8 rows x 64 k = 1 KiB) per wave and k-tile; a 32-row A image has 4 pieces for
+  // 8 waves: waves 4-7 load the same pieces as waves 0-3 (identical bytes to the same LDS words), so
+  // every wave issues the same count and the counted waits stay uniform
+  constexpr int APC = TBM / 8;
+  constexpr int PA = APC >= NW ? APC / NW : 1, PB = TBN / 8 / NW;
   constexpr int NMF = MI * NI;      // MFMAs per k-step
   constexpr int NRD = MI + NI;      // fragment reads per k-step
   // f32 outputs park each 8-row half block in LDS and store whole 128-B lines (the direct
@@ -1095,7 +1135,8 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   // ---- load stream: a wave issues LDS-DMA pieces wid*PA + p (A) and wid*PB + p (B) of the images (8 rows x 64 k
   // = 1 KiB each; 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)); source rows clamped (tails
   // re-read the last row, never stored)
-  const int prowa = wid * PA * 8 + (lane >> 3), prowb = wid * PB * 8 + (lane >> 3);  // + p * 8
+  const int prowa = ((wid * PA) % APC) * 8 + (lane >> 3), prowb = wid * PB * 8 + (lane >> 3);  // + p * 8
+  const int pieca = (wid * PA) % APC;  // first A piece of this wave
   // load-stream state: the k-tile the next issue_cur() loads (tile ld_it of this workgroup, k-tile
   // ld_kt of it); per tile, uniform row-block bases and per-lane 32-bit element offsets
   // (two streams, A and B: with AR the A stream runs one k-tile ahead, otherwise in lockstep)
@@ -1127,7 +1168,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     const __bf16* pa = ldA + la_kt * BK;
 #pragma unroll
     for (int p = 0; p < PA; ++p)
-      __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + slot * ASTAGE + (wid * PA + p) * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + slot * ASTAGE + (pieca + p) * 512), 16, 0, 0);
   };
   auto issue_b = [&](int slot) {
     const __bf16* pb = ldB + lb_kt * BK;
@@ -1147,7 +1188,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 #pragma unroll
       for (int p = 0; p < (PA > PB ? PA : PB); ++p) {
         if (p < PA)
-          __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + aslot * ASTAGE + (wid * PA + p) * 512), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + aslot * ASTAGE + (pieca + p) * 512), 16, 0, 0);
         if (p < PB)
           __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]),
                                            (lds_void*)(smem + BRING + bslot * BSTAGE + (wid * PB + p) * 512), 16, 0, 0);
@@ -1824,7 +1865,7 @@ void pp_tile(const comet_gemm_args& a, int& tbm, int& tbn) {
 }
 
 // Row-LN launch (comet_gemm_rowln): f32 output with a residual, no activation / aux, one tile
-// spanning the row. Instances: 128 x 384 / 64 x 384 (N = 384), 128 x 256 (N = 256).
+// spanning the row. Instances: 128 x 384 / 64 x 384 / 32 x 384 (N = 384), 128 x 256 (N = 256).
 int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, a.alpha, COMET_ACT_NONE, 1};
   e.prio = getenv("COMET_GEMM_PRIO") != nullptr;
@@ -1836,6 +1877,9 @@ int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s
   // (the full-height LN instances run at 256 VGPRs with spills; tools/rowln_bench.py)
   const bool full = tbn == 384 && a.k >= 1024 && getenv("COMET_ROWLN_HALF") == nullptr;
   if (!full && tbm == (tbn == 384 ? 128 : 256)) tbm /= 2;
+  // quarter-height 32 x 384 tiles when the 64-row grid fills at most half the CUs (M = 8192: the
+  // tracker's virtual tracks): every CU gets a tile
+  if (tbn == 384 && tbm == 64 && 2 * cdiv(a.m, 64) <= grid && getenv("COMET_ROWLN_NO32") == nullptr) tbm = 32;
   const int64_t tiles_m = cdiv(a.m, tbm);
   COMET_CHECK_ARG(tbn == a.n && tiles_m < (1ll << 30), "comet_gemm_rowln: the row must fit one tile");
   const int ntiles = (int)tiles_m;
@@ -1844,7 +1888,7 @@ int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s
   hipLaunchKernelGGL((w4::gemm_w4_kernel<float, COMET_ACT_NONE, true, 8, BMT, BNT, true>), dim3((unsigned)grid), \
                      dim3(512), 0, s, (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (float*)a.c, a.ldc,  \
                      a.m, a.n, a.k, 1, ntiles, e, ln)
-  if (tbn == 384) { if (tbm == 64) PPLN(64, 384); else PPLN(128, 384); }
+  if (tbn == 384) { if (tbm == 32) PPLN(32, 384); else if (tbm == 64) PPLN(64, 384); else PPLN(128, 384); }
   else PPLN(128, 256);
 #undef PPLN
   COMET_CHECK_LAUNCH("comet_gemm_rowln (persistent, row LN epilogue)");
@@ -2663,6 +2707,67 @@ extern "C" int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_a
   w4::RowLN r{reinterpret_cast<__bf16*>(ln->y16), ln->ldy, ln->eps_y, reinterpret_cast<__bf16*>(ln->z16), ln->ldz,
               ln->zw, ln->zb, ln->eps_z, ln->raw_c};
   return launch_pp_rowln(*args, r, as_stream(stream));
+}
+
+// ---- GEMM + activation backward (comet_gemm_dact) --------------------------------------------
+// dPre = act'(pre) * (A.B) in bf16 with the bias gradient dcol = column sums of dPre: the
+// hidden-layer gradient of an MLP (fc2's dX GEMM fused with fc1's GELU backward and bias gradient),
+// on the 256-row kernel without split-K.
+namespace comet {
+namespace {
+bool dact_ok(const comet_gemm_args& a, int act, const void* pre, int64_t ldpre) {
+  if (act != COMET_ACT_GELU || a.dtype_ab != COMET_BF16 || a.dtype_c != COMET_BF16 || a.layout_a != 0) return false;
+  if (a.bias || a.resid || a.aux || a.act != COMET_ACT_NONE || a.batch[0] * a.batch[1] != 1) return false;
+  if (a.n % 8 != 0 || (uintptr_t)a.c % 16 != 0 || a.ldc % 8 != 0) return false;
+  if (pre == nullptr || (uintptr_t)pre % 16 != 0 || ldpre % 8 != 0 || ldpre < a.n) return false;
+  const int bn = big_bn(a);
+  if (bn == 0 || a.k % 64 != 0) return false;
+  const int64_t tiles = cdiv(a.m, big::BM) * cdiv(a.n, bn);
+  return !(tiles < kCUs && a.k / 64 >= 16);  // make_plan would split K: not fused
+}
+
+template <int BN, int LB>
+int launch_big_dact(const comet_gemm_args& a, const __bf16* pre, int64_t ldpre, float* dcol, hipStream_t s) {
+  Epi e{nullptr, 0, 0, 0, nullptr, 0, 0, 0, 0.f, nullptr, 0, 0, 0, a.alpha, COMET_ACT_NONE, 1};
+  e.gpre = pre; e.ldg = ldpre; e.dcol = dcol;
+  const int64_t tiles_m = cdiv(a.m, big::BM), tiles_n = cdiv(a.n, BN);
+  COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 31), "comet_gemm_dact: too many tiles");
+  if (dcol != nullptr && hipMemsetAsync(dcol, 0, a.n * sizeof(float), s) != hipSuccess) {
+    set_error("comet_gemm_dact: memset failed");
+    return COMET_ELAUNCH;
+  }
+  Split sp{nullptr, a.k};
+  hipLaunchKernelGGL((big::gemm_big_kernel<__bf16, BN, 0, LB, false, 0, true>), dim3((unsigned)(tiles_m * tiles_n)),
+                     dim3(big::NT), 0, s, (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (__bf16*)a.c, a.ldc,
+                     a.m, a.n, a.k, (int)tiles_n, e, sp);
+  COMET_CHECK_LAUNCH("comet_gemm_dact");
+  return COMET_OK;
+}
+}  // namespace
+}  // namespace comet
+
+extern "C" int comet_gemm_dact_ok(const comet_gemm_args* args, int32_t act, const void* pre, int64_t ldpre) {
+  using namespace comet;
+  if (args == nullptr || validate(args) != COMET_OK) return 0;
+  return dact_ok(*args, act, pre, ldpre) ? 1 : 0;
+}
+
+extern "C" int comet_gemm_dact(const comet_gemm_args* args, int32_t act, const void* pre, int64_t ldpre, float* dbias,
+                               void* stream) {
+  using namespace comet;
+  const int rc = validate(args);
+  if (rc != COMET_OK) return rc;
+  COMET_CHECK_ARG(args->a && args->b && args->c, "comet_gemm_dact: null operand");
+  COMET_CHECK_ARG(dact_ok(*args, act, pre, ldpre), "comet_gemm_dact: not eligible (GELU, bf16 operands and output, "
+                                                   "A k-contiguous, no bias / residual / aux / activation, one batch, "
+                                                   "N % 8 == 0, 16-B aligned C and pre, a 256-row tile plan without split-K)");
+  if (args->m == 0) return COMET_OK;
+  const comet_gemm_args& a = *args;
+  const __bf16* pre16 = reinterpret_cast<const __bf16*>(pre);
+  hipStream_t s = as_stream(stream);
+  const int bn = big_bn(a);
+  if (bn == 256) return a.layout_b ? launch_big_dact<256, 1>(a, pre16, ldpre, dbias, s) : launch_big_dact<256, 0>(a, pre16, ldpre, dbias, s);
+  return a.layout_b ? launch_big_dact<128, 1>(a, pre16, ldpre, dbias, s) : launch_big_dact<128, 0>(a, pre16, ldpre, dbias, s);
 }
 
 #ifdef COMET_GEMM_STAMPS

@@ -770,10 +770,11 @@ extern "C" int comet_corr_sample(int dtype_fmap, int dtype_feat, const void* con
     COMET_CHECK_ARG(grid < (1ll << 31) && N < (1ll << 30), "comet_corr_sample: too many tracks");
     const char* rs = std::getenv("COMET_CORR_RING");
     const int ring = rs ? std::atoi(rs) : 2;
-    const bool occ4 = std::getenv("COMET_CORR_OCC4") != nullptr;
+    // default: the 2-deep ring at 4 waves per SIMD (128 VGPRs; 242 vs 274 us at 3 waves, profiles/r04_corr)
+    const bool occ3 = std::getenv("COMET_CORR_OCC3") != nullptr || rs != nullptr;
 #define CM(R, O) hipLaunchKernelGGL((corr_mfma_kernel<128, R, O>), dim3((unsigned)grid), dim3(256), lds, s, tab, levels, \
                                     radius, (const float*)feats, coords, out, ldo, col0, (int)N, S, (int)frames, isc, sort)
-    if (occ4) CM(2, 4); else if (ring >= 4) CM(4, 1); else if (ring == 3) CM(3, 1); else CM(2, 1);
+    if (!occ3) CM(2, 4); else if (ring >= 4) CM(4, 1); else if (ring == 3) CM(3, 1); else CM(2, 1);
 #undef CM
     COMET_CHECK_LAUNCH("comet_corr_sample");
     return COMET_OK;

@@ -106,6 +106,19 @@ typedef struct comet_rowln_args {
 int comet_gemm_rowln_ok(const comet_gemm_args* args);
 int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_args* ln, void* stream);
 
+/* GEMM + activation backward (Mlp.fc2's input gradient fused with fc1's GELU backward and bias
+ * gradient, modules.py:18-40 / timm Mlp under loss.backward(), train_eval_func_new_cp5.py:793):
+ *   c[m, n]   = bf16( act'(pre[m, n]) * alpha * sum_k A[m, k] B[k, n] )     (act = GELU, erf form)
+ *   dbias[n]  = sum_m c[m, n]   (the rounded values; zeroed first; may be NULL)
+ * pre: bf16 [M, N] at row pitch ldpre (fc1's saved pre-activation). Replaces the dX GEMM + the
+ * comet_act_bwd_colsum pass (the hidden gradient is written once instead of written, read and
+ * written again). Eligible (comet_gemm_dact_ok): act GELU, bf16 A / B / C, A k-contiguous, no bias,
+ * residual, aux or forward activation, one batch, N % 8 == 0, 16-B aligned C and pre, a 256-row
+ * tile plan (comet_gemm_plan kind 1) without split-K. */
+int comet_gemm_dact_ok(const comet_gemm_args* args, int32_t act, const void* pre, int64_t ldpre);
+int comet_gemm_dact(const comet_gemm_args* args, int32_t act, const void* pre, int64_t ldpre, float* dbias,
+                    void* stream);
+
 
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM convolution on channels-last activations (nn.Conv2d of BasicEncoder /

@@ -798,6 +798,68 @@ def test_corr_sample_vs_f64(C, radius, dtype):
     assert (out[:, :2] == 7.0).all() and (out[:, 2 + levels * win * win:] == 7.0).all()
 
 
+@pytest.mark.parametrize("M,N2,K2", [(4133, 256, 1024), (8192, 768, 3072)])
+def test_gemm_dact_vs_torch(M, N2, K2):
+    """comet_gemm_dact: dPre = GELU'(pre) * (dY @ W) in bf16 and dbias = column sums of the stored
+    values, against torch in f32 (the erf GELU derivative) on the same bf16 operands; the bias
+    gradient against the column sums of our own bf16 output (what the next GEMMs consume)."""
+    ops = _ops()
+    from comet_amd import _lib as L
+    g = torch.Generator().manual_seed(M + N2)
+    dy = (torch.randn(M, N2, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(N2, K2, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    pre = (torch.randn(M, K2, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    assert ops.linear_dact_ok(dy, w, pre, L.ACT_GELU)
+    db = torch.full((K2,), 5.0, device=DEV)
+    out = ops.linear_dact(dy, w, pre, L.ACT_GELU, dbias=db)
+    x = pre.double()
+    gelu_d = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+    ref = (dy.double() @ w.double()) * gelu_d
+    _close(out, ref, 8e-3, 1e-4 * ref.abs().max().item(), f"dact {M}x{N2}x{K2}")
+    cs = out.double().sum(0)
+    _close(db, cs, 1e-5, 1e-5 * cs.abs().max().item(), "dact dbias")
+    # not eligible: a pre-activation of another shape, or few output tiles over a short K (the
+    # 256-row kernel would not take the GEMM; the Mlp node then runs GEMM + comet_act_bwd_colsum)
+    assert not ops.linear_dact_ok(dy, w, pre[:, :K2 - 8], L.ACT_GELU)
+    assert not ops.linear_dact_ok(dy[:300], w, pre[:300], L.ACT_GELU)
+
+
+@pytest.mark.parametrize("rows", [8 * 577, 128])
+def test_mlp_fused_backward_matches_unfused(monkeypatch, rows):
+    """The camera head's Mlp as one autograd node (fc2's input gradient fused with fc1's GELU
+    backward, comet_gemm_dact) against the two-Linear path (GEMM + comet_act_bwd_colsum) at a
+    T_P-like shape in bf16: the forward is the same kernels (bit-identical); the gradients differ
+    by one bf16 rounding of the hidden gradient (the fused path rounds once). 128 rows (the camera
+    trunk's token count) take the node's unfused fallback."""
+    _ops()
+    from comet_amd import functional as F
+    from comet_amd.models.modules import Mlp
+    torch.manual_seed(0)
+    mlp = Mlp(768, 3072).to(DEV)
+    x0 = torch.randn(rows, 768, device=DEV)
+    r0 = torch.randn(rows, 768, device=DEV)
+    outs = {}
+    for fused in (True, False):
+        monkeypatch.setattr(F, "_MLP_UNFUSED", not fused)
+        mlp.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        r = r0.clone().requires_grad_(True)
+        with F.precision(torch.bfloat16):
+            y = mlp(x, resid=r)
+        (y * torch.linspace(-1, 1, 768, device=DEV)).sum().backward()
+        outs[fused] = (y.detach(), x.grad, r.grad, mlp.fc1.weight.grad, mlp.fc1.bias.grad, mlp.fc2.weight.grad,
+                       mlp.fc2.bias.grad)
+    names = ("y", "dx", "dresid", "dw1", "db1", "dw2", "db2")
+    for n, a, b in zip(names, outs[True], outs[False]):
+        if n in ("y", "dresid", "dw2"):
+            assert torch.equal(a, b), n
+        elif n == "db2":  # column sums by float atomics: summation order only
+            assert ((a - b).abs().max() <= 1e-5 * b.abs().max()).item(), n
+        else:
+            rel = ((a.float() - b.float()).norm() / b.float().norm()).item()
+            assert rel < 1e-2, (n, rel)
+
+
 @pytest.mark.parametrize("layout", ["uniform", "clustered", "outside"])
 def test_corr_sample_mfma_vs_f64(layout):
     """The matrix-core CorrBlock path (bf16 maps, C = 128, >= 16 tracks per frame: the coarse

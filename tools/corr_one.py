@@ -1,5 +1,5 @@
 """A few comet_corr_sample launches at the coarse tracker's shape (B=8, S=16, N=512, 64^2 x 128
-bf16, 4 levels, r=4), for rocprofv3 counter passes (tools/gpu/corr_pmc.sh)."""
+bf16, 4 levels, r=4), for rocprofv3 counter passes (tools/gpu/prog_pmc.sh <tag> tools/corr_one.py)."""
 import os
 import sys
 
