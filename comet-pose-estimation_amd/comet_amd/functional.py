@@ -298,15 +298,16 @@ class _Mlp(torch.autograd.Function):
 
 
 def mlp(x, w1, b1, w2, b2, resid=None, out_dtype=torch.float32):
-    """fc2(GELU(fc1(x))) (+ resid). In bf16 compute with gradients one autograd node (_Mlp); the
-    fused backward can be switched off with COMET_NO_MLP_FUSE=1 (A/B)."""
+    """fc2(GELU(fc1(x))) (+ resid). With COMET_MLP_FUSE=1, in bf16 compute with gradients, one
+    autograd node (_Mlp) whose backward fuses fc1's GELU backward into fc2's input-gradient GEMM;
+    otherwise two Linear nodes (the default until the fused node is measured on the GPU)."""
     if compute_dtype() == torch.bfloat16 and _needs_grad(x, w1, b1, w2, b2, resid) and not _MLP_UNFUSED:
         return _Mlp.apply(x, w1, b1, w2, b2, resid, out_dtype)
     h = linear(x, w1, b1, act=L.ACT_GELU)
     return linear(h, w2, b2, resid=resid, out_dtype=out_dtype)
 
 
-_MLP_UNFUSED = os.environ.get("COMET_NO_MLP_FUSE") is not None
+_MLP_UNFUSED = os.environ.get("COMET_MLP_FUSE") is None
 
 
 # ------------------------------------------------------------------------------------------

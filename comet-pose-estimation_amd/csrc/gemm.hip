@@ -1878,8 +1878,8 @@ int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s
   const bool full = tbn == 384 && a.k >= 1024 && getenv("COMET_ROWLN_HALF") == nullptr;
   if (!full && tbm == (tbn == 384 ? 128 : 256)) tbm /= 2;
   // quarter-height 32 x 384 tiles when the 64-row grid fills at most half the CUs (M = 8192: the
-  // tracker's virtual tracks): every CU gets a tile
-  if (tbn == 384 && tbm == 64 && 2 * cdiv(a.m, 64) <= grid && getenv("COMET_ROWLN_NO32") == nullptr) tbm = 32;
+  // tracker's virtual tracks): every CU gets a tile. Opt-in (COMET_ROWLN_32=1) until measured on the GPU
+  if (tbn == 384 && tbm == 64 && 2 * cdiv(a.m, 64) <= grid && getenv("COMET_ROWLN_32") != nullptr) tbm = 32;
   const int64_t tiles_m = cdiv(a.m, tbm);
   COMET_CHECK_ARG(tbn == a.n && tiles_m < (1ll << 30), "comet_gemm_rowln: the row must fit one tile");
   const int ntiles = (int)tiles_m;

@@ -826,8 +826,8 @@ def test_gemm_dact_vs_torch(M, N2, K2):
 
 @pytest.mark.parametrize("rows", [8 * 577, 128])
 def test_mlp_fused_backward_matches_unfused(monkeypatch, rows):
-    """The camera head's Mlp as one autograd node (fc2's input gradient fused with fc1's GELU
-    backward, comet_gemm_dact) against the two-Linear path (GEMM + comet_act_bwd_colsum) at a
+    """The camera head's Mlp as one autograd node (COMET_MLP_FUSE=1: fc2's input gradient fused with
+    fc1's GELU backward, comet_gemm_dact) against the two-Linear path (GEMM + comet_act_bwd_colsum) at a
     T_P-like shape in bf16: the forward is the same kernels (bit-identical); the gradients differ
     by one bf16 rounding of the hidden gradient (the fused path rounds once). 128 rows (the camera
     trunk's token count) take the node's unfused fallback."""
@@ -1079,6 +1079,31 @@ def test_gemm_rowln_matches_separate_kernels():
     _close(c, y32r, 1e-5, 1e-5, "rowln dual f32 vs separate")
     d = (y16.float() - y16r.float()).abs() / y16r.float().abs().clamp_min(1e-3)
     assert d.max().item() <= 2 ** -7, d.max().item()
+
+
+@pytest.mark.parametrize("M,K", [(8192, 384), (8192, 1536), (8192 - 40, 1536), (4096 + 8, 384)])
+def test_gemm_rowln_32row_tiles(M, K, monkeypatch):
+    """32 x 384 row-LN tiles (COMET_ROWLN_32=1: M where the 64-row grid fills at most half the CUs;
+    four A pieces per k-tile, waves 4-7 load the same pieces as waves 0-3) equal the 64 x 384 tiles:
+    f32 dual copy within summation-order noise (the same k order per element: bit-equal expected),
+    both bf16 LayerNorms; M tails."""
+    ops = _ops()
+    N = 384
+    x = _rand(M, K, seed=121).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=122, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
+    b = _rand(N, seed=123, scale=0.1).to(DEV)
+    r = _rand(M, N, seed=124).to(DEV)
+    zw, zb = (1 + _rand(N, seed=125, scale=0.1)).to(DEV), _rand(N, seed=126, scale=0.1).to(DEV)
+    outs = []
+    for v32 in (False, True):
+        if v32:
+            monkeypatch.setenv("COMET_ROWLN_32", "1")
+        outs.append(ops.linear_rowln(x, w, b, r, raw=False, y16_eps=1e-6, z=(zw, zb, 1e-5)))
+    for a, c, what in zip(outs[1], outs[0], ("c", "y16", "z16")):
+        _close(a, c.double(), 1e-5 if what == "c" else 8e-3, 1e-5 if what == "c" else 8e-3, f"rowln 32 vs 64 {what} M{M} K{K}")
+    v = x.double() @ w.double().t() + b.double() + r.double()
+    ln = (v - v.mean(1, keepdim=True)) / torch.sqrt(v.var(1, unbiased=False, keepdim=True) + 1e-6)
+    _close(outs[1][0], ln, 1e-4, 1e-4, "rowln 32 vs f64")
 
 
 @pytest.mark.parametrize("mnk", [(8192, 1536, 384), (4096 + 72, 3072, 768), (65536, 1024, 256)])
