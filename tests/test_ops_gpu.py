@@ -798,68 +798,6 @@ def test_corr_sample_vs_f64(C, radius, dtype):
     assert (out[:, :2] == 7.0).all() and (out[:, 2 + levels * win * win:] == 7.0).all()
 
 
-@pytest.mark.parametrize("M,N2,K2", [(4133, 256, 1024), (8192, 768, 3072)])
-def test_gemm_dact_vs_torch(M, N2, K2):
-    """comet_gemm_dact: dPre = GELU'(pre) * (dY @ W) in bf16 and dbias = column sums of the stored
-    values, against torch in f32 (the erf GELU derivative) on the same bf16 operands; the bias
-    gradient against the column sums of our own bf16 output (what the next GEMMs consume)."""
-    ops = _ops()
-    from comet_amd import _lib as L
-    g = torch.Generator().manual_seed(M + N2)
-    dy = (torch.randn(M, N2, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
-    w = (torch.randn(N2, K2, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
-    pre = (torch.randn(M, K2, generator=g) * 2).to(torch.bfloat16).to(DEV)
-    assert ops.linear_dact_ok(dy, w, pre, L.ACT_GELU)
-    db = torch.full((K2,), 5.0, device=DEV)
-    out = ops.linear_dact(dy, w, pre, L.ACT_GELU, dbias=db)
-    x = pre.double()
-    gelu_d = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
-    ref = (dy.double() @ w.double()) * gelu_d
-    _close(out, ref, 8e-3, 1e-4 * ref.abs().max().item(), f"dact {M}x{N2}x{K2}")
-    cs = out.double().sum(0)
-    _close(db, cs, 1e-5, 1e-5 * cs.abs().max().item(), "dact dbias")
-    # not eligible: a pre-activation of another shape, or few output tiles over a short K (the
-    # 256-row kernel would not take the GEMM; the Mlp node then runs GEMM + comet_act_bwd_colsum)
-    assert not ops.linear_dact_ok(dy, w, pre[:, :K2 - 8], L.ACT_GELU)
-    assert not ops.linear_dact_ok(dy[:300], w, pre[:300], L.ACT_GELU)
-
-
-@pytest.mark.parametrize("rows", [8 * 577, 128])
-def test_mlp_fused_backward_matches_unfused(monkeypatch, rows):
-    """The camera head's Mlp as one autograd node (COMET_MLP_FUSE=1: fc2's input gradient fused with
-    fc1's GELU backward, comet_gemm_dact) against the two-Linear path (GEMM + comet_act_bwd_colsum) at a
-    T_P-like shape in bf16: the forward is the same kernels (bit-identical); the gradients differ
-    by one bf16 rounding of the hidden gradient (the fused path rounds once). 128 rows (the camera
-    trunk's token count) take the node's unfused fallback."""
-    _ops()
-    from comet_amd import functional as F
-    from comet_amd.models.modules import Mlp
-    torch.manual_seed(0)
-    mlp = Mlp(768, 3072).to(DEV)
-    x0 = torch.randn(rows, 768, device=DEV)
-    r0 = torch.randn(rows, 768, device=DEV)
-    outs = {}
-    for fused in (True, False):
-        monkeypatch.setattr(F, "_MLP_UNFUSED", not fused)
-        mlp.zero_grad(set_to_none=True)
-        x = x0.clone().requires_grad_(True)
-        r = r0.clone().requires_grad_(True)
-        with F.precision(torch.bfloat16):
-            y = mlp(x, resid=r)
-        (y * torch.linspace(-1, 1, 768, device=DEV)).sum().backward()
-        outs[fused] = (y.detach(), x.grad, r.grad, mlp.fc1.weight.grad, mlp.fc1.bias.grad, mlp.fc2.weight.grad,
-                       mlp.fc2.bias.grad)
-    names = ("y", "dx", "dresid", "dw1", "db1", "dw2", "db2")
-    for n, a, b in zip(names, outs[True], outs[False]):
-        if n in ("y", "dresid", "dw2"):
-            assert torch.equal(a, b), n
-        elif n == "db2":  # column sums by float atomics: summation order only
-            assert ((a - b).abs().max() <= 1e-5 * b.abs().max()).item(), n
-        else:
-            rel = ((a.float() - b.float()).norm() / b.float().norm()).item()
-            assert rel < 1e-2, (n, rel)
-
-
 @pytest.mark.parametrize("layout", ["uniform", "clustered", "outside"])
 def test_corr_sample_mfma_vs_f64(layout):
     """The matrix-core CorrBlock path (bf16 maps, C = 128, >= 16 tracks per frame: the coarse
@@ -1081,31 +1019,6 @@ def test_gemm_rowln_matches_separate_kernels():
     assert d.max().item() <= 2 ** -7, d.max().item()
 
 
-@pytest.mark.parametrize("M,K", [(8192, 384), (8192, 1536), (8192 - 40, 1536), (4096 + 8, 384)])
-def test_gemm_rowln_32row_tiles(M, K, monkeypatch):
-    """32 x 384 row-LN tiles (COMET_ROWLN_32=1: M where the 64-row grid fills at most half the CUs;
-    four A pieces per k-tile, waves 4-7 load the same pieces as waves 0-3) equal the 64 x 384 tiles:
-    f32 dual copy within summation-order noise (the same k order per element: bit-equal expected),
-    both bf16 LayerNorms; M tails."""
-    ops = _ops()
-    N = 384
-    x = _rand(M, K, seed=121).to(torch.bfloat16).to(DEV)
-    w = _rand(N, K, seed=122, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
-    b = _rand(N, seed=123, scale=0.1).to(DEV)
-    r = _rand(M, N, seed=124).to(DEV)
-    zw, zb = (1 + _rand(N, seed=125, scale=0.1)).to(DEV), _rand(N, seed=126, scale=0.1).to(DEV)
-    outs = []
-    for v32 in (False, True):
-        if v32:
-            monkeypatch.setenv("COMET_ROWLN_32", "1")
-        outs.append(ops.linear_rowln(x, w, b, r, raw=False, y16_eps=1e-6, z=(zw, zb, 1e-5)))
-    for a, c, what in zip(outs[1], outs[0], ("c", "y16", "z16")):
-        _close(a, c.double(), 1e-5 if what == "c" else 8e-3, 1e-5 if what == "c" else 8e-3, f"rowln 32 vs 64 {what} M{M} K{K}")
-    v = x.double() @ w.double().t() + b.double() + r.double()
-    ln = (v - v.mean(1, keepdim=True)) / torch.sqrt(v.var(1, unbiased=False, keepdim=True) + 1e-6)
-    _close(outs[1][0], ln, 1e-4, 1e-4, "rowln 32 vs f64")
-
-
 @pytest.mark.parametrize("mnk", [(8192, 1536, 384), (4096 + 72, 3072, 768), (65536, 1024, 256)])
 @pytest.mark.parametrize("act", [1, 2])
 def test_gemm_persistent_preact_bf16(mnk, act):
@@ -1153,3 +1066,91 @@ def test_gemm_small_split_matches_unsplit(la, lb, mnk, out, monkeypatch):
         _close(C, ref, q + 1e-5, 1e-4 * math.sqrt(K), f"{mode} {mnk} la={la} lb={lb} {out}")
     d = (res["split"] - res["nosplit"]).abs().max().item()
     assert d <= (2 * q + 1e-5) * ref.abs().max().item(), f"split vs unsplit differ by {d:.3e}"
+
+
+# ---- round 4, opt-in paths (COMET_MLP_FUSE=1, COMET_ROWLN_32=1); last in the file ----
+@pytest.mark.parametrize("M,N2,K2", [(4133, 256, 1024), (8192, 768, 3072)])
+def test_gemm_dact_vs_torch(M, N2, K2):
+    """comet_gemm_dact: dPre = GELU'(pre) * (dY @ W) in bf16 and dbias = column sums of the stored
+    values, against torch in f32 (the erf GELU derivative) on the same bf16 operands; the bias
+    gradient against the column sums of our own bf16 output (what the next GEMMs consume)."""
+    ops = _ops()
+    from comet_amd import _lib as L
+    g = torch.Generator().manual_seed(M + N2)
+    dy = (torch.randn(M, N2, generator=g) * 0.1).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(N2, K2, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    pre = (torch.randn(M, K2, generator=g) * 2).to(torch.bfloat16).to(DEV)
+    assert ops.linear_dact_ok(dy, w, pre, L.ACT_GELU)
+    db = torch.full((K2,), 5.0, device=DEV)
+    out = ops.linear_dact(dy, w, pre, L.ACT_GELU, dbias=db)
+    x = pre.double()
+    gelu_d = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+    ref = (dy.double() @ w.double()) * gelu_d
+    _close(out, ref, 8e-3, 1e-4 * ref.abs().max().item(), f"dact {M}x{N2}x{K2}")
+    cs = out.double().sum(0)
+    _close(db, cs, 1e-5, 1e-5 * cs.abs().max().item(), "dact dbias")
+    # not eligible: a pre-activation of another shape, or few output tiles over a short K (the
+    # 256-row kernel would not take the GEMM; the Mlp node then runs GEMM + comet_act_bwd_colsum)
+    assert not ops.linear_dact_ok(dy, w, pre[:, :K2 - 8], L.ACT_GELU)
+    assert not ops.linear_dact_ok(dy[:300], w, pre[:300], L.ACT_GELU)
+
+
+@pytest.mark.parametrize("rows", [8 * 577, 128])
+def test_mlp_fused_backward_matches_unfused(monkeypatch, rows):
+    """The camera head's Mlp as one autograd node (COMET_MLP_FUSE=1: fc2's input gradient fused with
+    fc1's GELU backward, comet_gemm_dact) against the two-Linear path (GEMM + comet_act_bwd_colsum) at a
+    T_P-like shape in bf16: the forward is the same kernels (bit-identical); the gradients differ
+    by one bf16 rounding of the hidden gradient (the fused path rounds once). 128 rows (the camera
+    trunk's token count) take the node's unfused fallback."""
+    _ops()
+    from comet_amd import functional as F
+    from comet_amd.models.modules import Mlp
+    torch.manual_seed(0)
+    mlp = Mlp(768, 3072).to(DEV)
+    x0 = torch.randn(rows, 768, device=DEV)
+    r0 = torch.randn(rows, 768, device=DEV)
+    outs = {}
+    for fused in (True, False):
+        monkeypatch.setattr(F, "_MLP_UNFUSED", not fused)
+        mlp.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        r = r0.clone().requires_grad_(True)
+        with F.precision(torch.bfloat16):
+            y = mlp(x, resid=r)
+        (y * torch.linspace(-1, 1, 768, device=DEV)).sum().backward()
+        outs[fused] = (y.detach(), x.grad, r.grad, mlp.fc1.weight.grad, mlp.fc1.bias.grad, mlp.fc2.weight.grad,
+                       mlp.fc2.bias.grad)
+    names = ("y", "dx", "dresid", "dw1", "db1", "dw2", "db2")
+    for n, a, b in zip(names, outs[True], outs[False]):
+        if n in ("y", "dresid", "dw2"):
+            assert torch.equal(a, b), n
+        elif n == "db2":  # column sums by float atomics: summation order only
+            assert ((a - b).abs().max() <= 1e-5 * b.abs().max()).item(), n
+        else:
+            rel = ((a.float() - b.float()).norm() / b.float().norm()).item()
+            assert rel < 1e-2, (n, rel)
+
+
+@pytest.mark.parametrize("M,K", [(8192, 384), (8192, 1536), (8192 - 40, 1536), (4096 + 8, 384)])
+def test_gemm_rowln_32row_tiles(M, K, monkeypatch):
+    """32 x 384 row-LN tiles (COMET_ROWLN_32=1: M where the 64-row grid fills at most half the CUs;
+    four A pieces per k-tile, waves 4-7 load the same pieces as waves 0-3) equal the 64 x 384 tiles:
+    f32 dual copy within summation-order noise (the same k order per element: bit-equal expected),
+    both bf16 LayerNorms; M tails."""
+    ops = _ops()
+    N = 384
+    x = _rand(M, K, seed=121).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=122, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
+    b = _rand(N, seed=123, scale=0.1).to(DEV)
+    r = _rand(M, N, seed=124).to(DEV)
+    zw, zb = (1 + _rand(N, seed=125, scale=0.1)).to(DEV), _rand(N, seed=126, scale=0.1).to(DEV)
+    outs = []
+    for v32 in (False, True):
+        if v32:
+            monkeypatch.setenv("COMET_ROWLN_32", "1")
+        outs.append(ops.linear_rowln(x, w, b, r, raw=False, y16_eps=1e-6, z=(zw, zb, 1e-5)))
+    for a, c, what in zip(outs[1], outs[0], ("c", "y16", "z16")):
+        _close(a, c.double(), 1e-5 if what == "c" else 8e-3, 1e-5 if what == "c" else 8e-3, f"rowln 32 vs 64 {what} M{M} K{K}")
+    v = x.double() @ w.double().t() + b.double() + r.double()
+    ln = (v - v.mean(1, keepdim=True)) / torch.sqrt(v.var(1, unbiased=False, keepdim=True) + 1e-6)
+    _close(outs[1][0], ln, 1e-4, 1e-4, "rowln 32 vs f64")
