@@ -1,7 +1,8 @@
 """Times comet_corr_sample at the coarse tracker's shape (B=8, S=16, N=512, 4 levels from 64^2,
 C=128, r=4) and the fine one (C=32, r=3 on 31x31 patch maps) for each dispatch variant: the
-matrix-core kernel with a 2 / 3 / 4-deep pixel ring (COMET_CORR_RING) and the VALU kernel
-(COMET_CORR_VALU=1); max difference against the first variant.
+matrix-core kernel at 4 waves per SIMD (default), at 3 (COMET_CORR_OCC3=1) and with a 3 / 4-deep
+pixel ring (COMET_CORR_RING, 3 waves per SIMD), and the VALU kernel (COMET_CORR_VALU=1); max
+difference against the first variant.
 
     python tools/corr_bench.py > gpurun_out/corr_bench.txt
 """
@@ -13,8 +14,8 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "comet-pose-estimation_amd"))
 from comet_amd import ops  # noqa: E402
 
-VARIANTS = [("mfma ring2", {}), ("mfma ring3", {"COMET_CORR_RING": "3"}), ("mfma ring4", {"COMET_CORR_RING": "4"}),
-            ("mfma occ4", {"COMET_CORR_OCC4": "1"}), ("valu", {"COMET_CORR_VALU": "1"})]
+VARIANTS = [("mfma occ4", {}), ("mfma occ3", {"COMET_CORR_OCC3": "1"}), ("mfma ring3", {"COMET_CORR_RING": "3"}),
+            ("mfma ring4", {"COMET_CORR_RING": "4"}), ("valu", {"COMET_CORR_VALU": "1"})]
 
 
 def run(C, r, B, N, S, H0, levels, reps=10, clustered=False):
@@ -30,7 +31,7 @@ def run(C, r, B, N, S, H0, levels, reps=10, clustered=False):
     out = torch.empty(rows, levels * win * win, device="cuda")
     first = None
     for name, env in VARIANTS:
-        for k in ("COMET_CORR_RING", "COMET_CORR_VALU", "COMET_CORR_OCC4"):
+        for k in ("COMET_CORR_RING", "COMET_CORR_VALU", "COMET_CORR_OCC3"):
             os.environ.pop(k, None)
         os.environ.update(env)
         ops.corr_sample(pyr, r, feats, coords, out, 0, B, N, S)
@@ -49,7 +50,7 @@ def run(C, r, B, N, S, H0, levels, reps=10, clustered=False):
         d = (out - first).abs().max().item()
         print(f"C={C} r={r} rows={rows}{' clustered' if clustered else ''} {name:11s}: {min(ts):7.1f} us  max diff {d:.2e}",
               flush=True)
-    for k in ("COMET_CORR_RING", "COMET_CORR_VALU", "COMET_CORR_OCC4"):
+    for k in ("COMET_CORR_RING", "COMET_CORR_VALU", "COMET_CORR_OCC3"):
         os.environ.pop(k, None)
 
 
