@@ -39,6 +39,9 @@ class GradBucketer:
         self.arrival = []
         self.launch_log = []  # (bucket, during_backward) of the last step, for tests / tracing
         self.in_backward = False
+        # a backward outside prepare_backward / finish_backward raises unless `local` is set (the
+        # bench's timing pass without the exchange): an unreduced gradient would let ranks diverge
+        self.local = False
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
     # ---------------------------------------------------------------------------------------
@@ -126,9 +129,13 @@ class GradBucketer:
         self.works.append((bi, dist.all_reduce(self.flat[bi], op=op, group=self.group, async_op=True)))
 
     def _on_grad(self, p):
-        # outside prepare_backward / finish_backward a backward stays local (no bucket, no
-        # collective): bench.py times the step that way to price the exposed all-reduce
-        if not self.in_backward or p in self.arrived:
+        if not self.in_backward:
+            if self.local:  # explicit opt-in: the backward stays local (no bucket, no collective)
+                return
+            raise RuntimeError("GradBucketer: a gradient arrived outside prepare_backward/finish_backward "
+                               "(use the accelerator's backward, or set bucketer.local = True for a "
+                               "deliberately rank-local backward)")
+        if p in self.arrived:
             return
         self.arrived.add(p)
         self.arrival.append(p)

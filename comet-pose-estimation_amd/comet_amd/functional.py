@@ -265,8 +265,8 @@ class _Mlp(torch.autograd.Function):
         x2, h, aux, w1, w2 = ctx.saved_tensors
         N = w2.shape[0]
         dy2 = dy.reshape(-1, N)
-        if not dy2.is_contiguous():
-            dy2 = dy2.contiguous()
+        if not _vec8(dy2):  # the colsum kernels need 8-column rows at 32-B alignment (N % 8: mlp())
+            dy2 = dy2.clone(memory_format=torch.contiguous_format)
         wc1, wc2 = wcast(w1, torch.bfloat16), wcast(w2, torch.bfloat16)
         ni = ctx.needs_input_grad
         # fc2: the bf16 operand of its two GEMMs and its bias gradient in one pass, then dW2 (its dX
@@ -301,7 +301,10 @@ def mlp(x, w1, b1, w2, b2, resid=None, out_dtype=torch.float32):
     """fc2(GELU(fc1(x))) (+ resid). With COMET_MLP_FUSE=1, in bf16 compute with gradients, one
     autograd node (_Mlp) whose backward fuses fc1's GELU backward into fc2's input-gradient GEMM;
     otherwise two Linear nodes (the default until the fused node is measured on the GPU)."""
-    if compute_dtype() == torch.bfloat16 and _needs_grad(x, w1, b1, w2, b2, resid) and not _MLP_UNFUSED:
+    # (the fused node's column-sum kernels need widths that are multiples of 8: the GAPR quaternion
+    # head's Mlp 768 -> 1536 -> 4 stays on the two-Linear path)
+    if (compute_dtype() == torch.bfloat16 and _needs_grad(x, w1, b1, w2, b2, resid) and not _MLP_UNFUSED
+            and w1.shape[0] % 8 == 0 and w2.shape[0] % 8 == 0):
         return _Mlp.apply(x, w1, b1, w2, b2, resid, out_dtype)
     h = linear(x, w1, b1, act=L.ACT_GELU)
     return linear(h, w2, b2, resid=resid, out_dtype=out_dtype)

@@ -283,8 +283,12 @@ class CometAccelerator:
         """Rank src's parameters and buffers to every rank, in state_dict order (one broadcast per
         tensor; runs once, at prepare)."""
         import torch.distributed as dist
-        for t in list(model.parameters()) + list(model.buffers()):
+        from . import functional as F
+        params = list(model.parameters())
+        for t in params + list(model.buffers()):
             dist.broadcast(t.data, src)
+        # the broadcast writes through .data (no version bump): drop compute-dtype copies cast before it
+        F.invalidate_weight_cache(params)
 
     def backward(self, loss):
         if self.ddp is not None:

@@ -868,7 +868,7 @@ def _gather_bytes(name, args, out):
     nb = lambda t: t.numel() * t.element_size()  # noqa: E731
     if name == "sample_bilinear":   # 4 bilinear corners per output value
         fmap, coords = args[0], args[1]
-        return 4 * nb(out) // 4 * fmap.element_size() + nb(coords) + nb(out)
+        return 4 * out.numel() * fmap.element_size() + nb(coords) + nb(out)
     if name == "track_score":       # (2r+1)^2 window of each track's patch feature map
         qfeat, pfeat, fine = args[0], args[1], args[2]
         r = args[6] if len(args) > 6 else 2

@@ -1135,8 +1135,14 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   // ---- load stream: a wave issues LDS-DMA pieces wid*PA + p (A) and wid*PB + p (B) of the images (8 rows x 64 k
   // = 1 KiB each; 16-B chunk c of row r stored at c ^ ((r >> 1) & 7)); source rows clamped (tails
   // re-read the last row, never stored)
-  const int prowa = ((wid * PA) % APC) * 8 + (lane >> 3), prowb = wid * PB * 8 + (lane >> 3);  // + p * 8
-  const int pieca = (wid * PA) % APC;  // first A piece of this wave
+  // first A piece of this wave: the wrap is compile-time absent unless the A image has fewer pieces
+  // than waves (32-row tiles), so the other instances keep the plain wid * PA addressing
+#ifdef COMET_APIECE_WRAP_ALL  // round-4 form (wrap in every instance; A/B build only, profiles/r05_rowln)
+  const int pieca = (wid * PA) % APC;
+#else
+  const int pieca = APC < NW ? (wid * PA) % APC : wid * PA;
+#endif
+  const int prowa = pieca * 8 + (lane >> 3), prowb = wid * PB * 8 + (lane >> 3);  // + p * 8
   // load-stream state: the k-tile the next issue_cur() loads (tile ld_it of this workgroup, k-tile
   // ld_kt of it); per tile, uniform row-block bases and per-lane 32-bit element offsets
   // (two streams, A and B: with AR the A stream runs one k-tile ahead, otherwise in lockstep)
@@ -1878,8 +1884,9 @@ int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s
   const bool full = tbn == 384 && a.k >= 1024 && getenv("COMET_ROWLN_HALF") == nullptr;
   if (!full && tbm == (tbn == 384 ? 128 : 256)) tbm /= 2;
   // quarter-height 32 x 384 tiles when the 64-row grid fills at most half the CUs (M = 8192: the
-  // tracker's virtual tracks): every CU gets a tile. Opt-in (COMET_ROWLN_32=1) until measured on the GPU
-  if (tbn == 384 && tbm == 64 && 2 * cdiv(a.m, 64) <= grid && getenv("COMET_ROWLN_32") != nullptr) tbm = 32;
+  // tracker's virtual tracks): every CU gets a tile. Default since round 5 (2-5 % faster on every
+  // M = 8192 shape, same box, profiles/r05_rowln); COMET_ROWLN_NO32=1 keeps the 64-row tiles
+  if (tbn == 384 && tbm == 64 && 2 * cdiv(a.m, 64) <= grid && getenv("COMET_ROWLN_NO32") == nullptr) tbm = 32;
   const int64_t tiles_m = cdiv(a.m, tbm);
   COMET_CHECK_ARG(tbn == a.n && tiles_m < (1ll << 30), "comet_gemm_rowln: the row must fit one tile");
   const int ntiles = (int)tiles_m;

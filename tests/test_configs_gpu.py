@@ -8,9 +8,12 @@ Appendix B-1). The cross-frame attention at this size (Lq = 63 x 577 = 36351 que
 checked against an f64 reference on sampled rows.
 
 configs[3] (DDP, global batch over ranks): two ranks on this one GPU (gloo process group on device
-tensors), each running the real model on its own sequence; after GradBucketer's all-reduce
-(average) every rank's camera-predictor gradients equal the single-process B=2 gradients
-(SURVEY §4 "simulated ranks")."""
+tensors), each running the real model on its own sequences; after GradBucketer's all-reduce
+(average) every rank's camera-predictor gradients equal the single-process gradients of both ranks'
+sequences together (SURVEY §4 "simulated ranks"). The `headline_B8` size runs configs[3]'s own
+per-rank workload (B = 8 per rank, T = 16, 512², N = 512, bf16: the bench's M = 73,856-row GEMM
+plans, 25 MB buckets discovered and rebuilt in the B = 8 backward order) against the single-process
+B = 16 run."""
 import os
 import socket
 
@@ -131,11 +134,14 @@ def _free_port():
     return port
 
 
-SIZES = {  # name -> (seed, T, image, N, dtype)
-    "golden": (31, 4, 128, 16, torch.float32),
+SIZES = {  # name -> (seed, T, image, N, dtype, sequences per rank)
+    "golden": (31, 4, 128, 16, torch.float32, 1),
     # the headline per-sequence workload (BASELINE configs[3] is configs[2] per rank): T=16, 512^2,
     # N=512, bf16 -- 2 ranks x B=1 against the single-process B=2
-    "headline": (37, 16, 512, 512, torch.bfloat16),
+    "headline": (37, 16, 512, 512, torch.bfloat16, 1),
+    # configs[3]'s per-rank batch (train_e2epose2.py:83 under accelerate, B = 8 per GPU): 2 ranks x
+    # B=8 against the single-process B=16
+    "headline_B8": (41, 16, 512, 512, torch.bfloat16, 8),
 }
 SELECT = ("fc_depth.weight", "trunk.3.mlp.fc2.weight", "pose_token", "self_att.0.attn.in_proj_weight",
           "cross_att.3.mlp.fc1.weight", "traj_encoder.mlp.3.weight")
@@ -143,8 +149,8 @@ SELECT = ("fc_depth.weight", "trunk.3.mlp.fc2.weight", "pose_token", "self_att.0
 
 def _inputs(size):
     from oracle import prng
-    seed, T, S, N, _ = SIZES[size]
-    return prng.synthetic_batch(seed, 2, T, S, S, N)
+    seed, T, S, N, _, br = SIZES[size]
+    return prng.synthetic_batch(seed, 2 * br, T, S, S, N)
 
 
 def _rank(rank, world, port, q, paths, size):
@@ -158,9 +164,12 @@ def _rank(rank, world, port, q, paths, size):
         from comet_amd import functional as F
         from comet_amd.ddp import GradBucketer
         model, cfg = _model()
-        T, dtype = SIZES[size][1], SIZES[size][4]
+        T, dtype, br = SIZES[size][1], SIZES[size][4], SIZES[size][5]
         img, tracks, gt = _inputs(size)
-        img, tracks, cams = img[rank:rank + 1].cuda(), tracks[rank:rank + 1].cuda(), _cams(_sub(gt, rank, T))
+        lo, hi = rank * br, (rank + 1) * br
+        img, tracks = img[lo:hi].cuda(), tracks[lo:hi].cuda()
+        cams = _cams({k: (v[lo * T:hi * T] if k != "ratio" else v) for k, v in gt.items()})
+        del gt
 
         def fwd_bwd():
             with F.precision(dtype):
@@ -187,6 +196,8 @@ def _rank(rank, world, port, q, paths, size):
             g = {k: p.grad.detach().cpu().numpy().copy() for k, p in model.camera_predictor.named_parameters()
                  if p.grad is not None and k in SELECT}
         during = all(d for _, d in bk.launch_log)
+        print(f"{size} rank {rank}: B={br}, {len(bk.buckets)} buckets, peak device memory "
+              f"{torch.cuda.max_memory_allocated() / 2**30:.1f} GiB", flush=True)
         q.put((rank, res, g, during, len(bk.buckets), local))
         dist.destroy_process_group()
     except Exception as e:  # surface the error to the parent
@@ -195,12 +206,12 @@ def _rank(rank, world, port, q, paths, size):
         raise
 
 
-@pytest.mark.parametrize("size", ["golden", "headline"])
+@pytest.mark.parametrize("size", ["golden", "headline", "headline_B8"])
 def test_ddp_simulated_ranks_equal_B2_gradients(size):
     """Every rank's all-reduced gradient (a) equals the mean of the two ranks' local gradients
-    (exact up to summation order: the exchange itself), and (b) equals the single-process B=2
-    gradient (batch independence of the model: fp32 1e-4; bf16 within the bf16 tolerance, as B=2
-    and B=1 take different GEMM tilings)."""
+    (exact up to summation order: the exchange itself), and (b) equals the single-process gradient
+    of both ranks' sequences (B=2, or B=16 for headline_B8: batch independence of the model: fp32
+    1e-4; bf16 within the bf16 tolerance, as the batch sizes take different GEMM tilings)."""
     from comet_amd import functional as F
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -224,7 +235,7 @@ def test_ddp_simulated_ranks_equal_B2_gradients(size):
             print(f"{size} rank {rank} {k}: reduced vs mean(local) rel-to-max {err:.2e}")
             assert err < 1e-5, (rank, k, err)
     # (b) single process, B = 2
-    seed, T, S, N, dtype = SIZES[size]
+    seed, T, S, N, dtype, _ = SIZES[size]
     model, cfg = _model()
     img, tracks, gt = _inputs(size)
     with F.precision(dtype):

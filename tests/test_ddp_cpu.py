@@ -219,7 +219,15 @@ def _local_worker(rank, world, port, q, paths):
             bk.finish_backward()
         net.zero_grad(set_to_none=True)
         x, y = _data(rank, 5)
-        ((net(x) - y) ** 2).mean().backward()  # outside prepare / finish: local gradients
+        try:  # outside prepare / finish without the opt-in: refused (ranks would diverge unnoticed)
+            ((net(x) - y) ** 2).mean().backward()
+            raise AssertionError("a backward outside prepare/finish was accepted without bucketer.local")
+        except RuntimeError as e:
+            assert "outside prepare_backward" in str(e)
+        net.zero_grad(set_to_none=True)
+        bk.local = True
+        ((net(x) - y) ** 2).mean().backward()  # explicit opt-in: local gradients
+        bk.local = False
         q.put((rank, {k: p.grad.numpy().copy() for k, p in net.named_parameters() if p.grad is not None},
                len(bk.launch_log)))
     finally:
@@ -227,8 +235,9 @@ def _local_worker(rank, world, port, q, paths):
 
 
 def test_backward_outside_prepare_stays_local():
-    """A backward outside prepare_backward / finish_backward launches no collective and leaves each
-    rank its own gradient (bench.py times the step that way to price the exposed all-reduce)."""
+    """A backward outside prepare_backward / finish_backward raises unless `bucketer.local` is set;
+    with it, it launches no collective and leaves each rank its own gradient (bench.py times the
+    step that way to price the exposed all-reduce)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

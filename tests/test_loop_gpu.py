@@ -103,8 +103,12 @@ def test_abl_ours_test_fn_end_to_end(tmp_path):
     assert list(r.keys()) == ["epoch", "it", "mode"] + list(loop.TO_PLOT_METRICS)
     from comet_amd.data import YTDataset
     n = len(YTDataset(str(root / "AMD_eval"), crop_size=[128, 128], seq_len=4, split="valid"))
-    # Stats "it": one per sample, plus the lr update test_fn makes after the pass (abl_ours.py:69)
-    assert r["mode"] == "eval" and int(r["epoch"]) == -1 and int(r["it"]) == n
+    assert r["mode"] == "eval" and int(r["epoch"]) == -1
+    # "it" is PARITY UNPINNED: its value comes from pytorch3d implicitron's Stats, the base class of
+    # the reference's VizStats (train_util.py:1914), which is not in the reference tree. What is
+    # asserted here is this build's own Stats semantics (one iteration per sample of the pass, plus
+    # the lr update test_fn makes after it, abl_ours.py:69), not a reference value.
+    assert int(r["it"]) == n
     for k in ("Auc_30", "R_avg", "T_avg", "acc@5deg_x", "lr"):
         v = float(r[k])
         assert v == v, k   # logged and not NaN

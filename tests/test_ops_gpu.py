@@ -1068,7 +1068,7 @@ def test_gemm_small_split_matches_unsplit(la, lb, mnk, out, monkeypatch):
     assert d <= (2 * q + 1e-5) * ref.abs().max().item(), f"split vs unsplit differ by {d:.3e}"
 
 
-# ---- round 4, opt-in paths (COMET_MLP_FUSE=1, COMET_ROWLN_32=1); last in the file ----
+# ---- round 4 paths: opt-in COMET_MLP_FUSE=1, the 32-row row-LN tiles (default since round 5); last in the file ----
 @pytest.mark.parametrize("M,N2,K2", [(4133, 256, 1024), (8192, 768, 3072)])
 def test_gemm_dact_vs_torch(M, N2, K2):
     """comet_gemm_dact: dPre = GELU'(pre) * (dY @ W) in bf16 and dbias = column sums of the stored
@@ -1133,10 +1133,10 @@ def test_mlp_fused_backward_matches_unfused(monkeypatch, rows):
 
 @pytest.mark.parametrize("M,K", [(8192, 384), (8192, 1536), (8192 - 40, 1536), (4096 + 8, 384)])
 def test_gemm_rowln_32row_tiles(M, K, monkeypatch):
-    """32 x 384 row-LN tiles (COMET_ROWLN_32=1: M where the 64-row grid fills at most half the CUs;
-    four A pieces per k-tile, waves 4-7 load the same pieces as waves 0-3) equal the 64 x 384 tiles:
-    f32 dual copy within summation-order noise (the same k order per element: bit-equal expected),
-    both bf16 LayerNorms; M tails."""
+    """32 x 384 row-LN tiles (the default since round 5 where the 64-row grid fills at most half
+    the CUs; four A pieces per k-tile, waves 4-7 load the same pieces as waves 0-3) equal the 64 x 384
+    tiles (COMET_ROWLN_NO32=1): f32 dual copy within summation-order noise (the same k order per
+    element: bit-equal expected), both bf16 LayerNorms; M tails."""
     ops = _ops()
     N = 384
     x = _rand(M, K, seed=121).to(torch.bfloat16).to(DEV)
@@ -1147,7 +1147,9 @@ def test_gemm_rowln_32row_tiles(M, K, monkeypatch):
     outs = []
     for v32 in (False, True):
         if v32:
-            monkeypatch.setenv("COMET_ROWLN_32", "1")
+            monkeypatch.delenv("COMET_ROWLN_NO32", raising=False)
+        else:
+            monkeypatch.setenv("COMET_ROWLN_NO32", "1")
         outs.append(ops.linear_rowln(x, w, b, r, raw=False, y16_eps=1e-6, z=(zw, zb, 1e-5)))
     for a, c, what in zip(outs[1], outs[0], ("c", "y16", "z16")):
         _close(a, c.double(), 1e-5 if what == "c" else 8e-3, 1e-5 if what == "c" else 8e-3, f"rowln 32 vs 64 {what} M{M} K{K}")
