@@ -298,9 +298,9 @@ class _Mlp(torch.autograd.Function):
 
 
 def mlp(x, w1, b1, w2, b2, resid=None, out_dtype=torch.float32):
-    """fc2(GELU(fc1(x))) (+ resid). With COMET_MLP_FUSE=1, in bf16 compute with gradients, one
-    autograd node (_Mlp) whose backward fuses fc1's GELU backward into fc2's input-gradient GEMM;
-    otherwise two Linear nodes (the default until the fused node is measured on the GPU)."""
+    """fc2(GELU(fc1(x))) (+ resid). In bf16 compute with gradients, one autograd node (_Mlp) whose
+    backward fuses fc1's GELU backward into fc2's input-gradient GEMM (COMET_MLP_UNFUSE=1: two Linear
+    nodes, the path the fp32 compute and no-grad forwards always take)."""
     # (the fused node's column-sum kernels need widths that are multiples of 8: the GAPR quaternion
     # head's Mlp 768 -> 1536 -> 4 stays on the two-Linear path)
     if (compute_dtype() == torch.bfloat16 and _needs_grad(x, w1, b1, w2, b2, resid) and not _MLP_UNFUSED
@@ -310,7 +310,9 @@ def mlp(x, w1, b1, w2, b2, resid=None, out_dtype=torch.float32):
     return linear(h, w2, b2, resid=resid, out_dtype=out_dtype)
 
 
-_MLP_UNFUSED = os.environ.get("COMET_MLP_FUSE") is None
+# default since round 5 (one node per Mlp: -1.1 ms/step, same box, profiles/r05_attn); COMET_MLP_UNFUSE=1
+# keeps two Linear nodes
+_MLP_UNFUSED = os.environ.get("COMET_MLP_UNFUSE") is not None
 
 
 # ------------------------------------------------------------------------------------------

@@ -261,7 +261,15 @@ attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, i
                      const __bf16* __restrict__ V, int64_t sv_b, int64_t sv_h, int64_t sv_l,
                      __bf16* __restrict__ O, int64_t so_b, int64_t so_h, int64_t so_l,
                      float* __restrict__ LSE, int heads, int lq, int lk, float scale_log2, Inner in) {
-  constexpr int DA = ((D + 31) / 32) * 32, KP = DA + 8;
+  constexpr int DA = ((D + 31) / 32) * 32;
+  // LDS row pitch: K is read by ds_read_b128 (lane (li, hg) takes row li, 16-B chunk 4c + hg; the
+  // four 16-lane groups {0-3,12-15,20-27}, ... each need 16 distinct 16-B slots of the 256-B bank row:
+  // slot = (KP / 8) li + hg + 4c mod 16), V by ds_read_b64_tr_b16 (rows 4 hg + qq of 8 dwords each per
+  // 32-lane half: distinct 8-dword windows mod 64). KP / 8 = 10 (DA <= 64) or 14 (DA = 96) satisfies
+  // both; the round-4 pitch DA + 8 (9 or 13 slots) put ~2 conflict cycles on every K read
+  // (SQ_LDS_BANK_CONFLICT 11.3 M for 5.7 M LDS instructions, profiles/r04_attn/pmc_fwd_d64.txt)
+  constexpr int KP = DA <= 64 ? 80 : 112;
+  static_assert(DA <= 96, "attn_fwd_bf16_kernel: D <= 96");
   constexpr int DT = (D + 15) / 16, NQC = DA / 32;
   constexpr int NVROW = D / 8, NVT = (64 * NVROW + 255) / 256;
   __shared__ __attribute__((aligned(16))) __bf16 Ks[64 * KP];
@@ -456,8 +464,12 @@ attn_fwd32_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
   static_assert(D % 16 == 0 && D <= 128, "D: multiple of 16");
   constexpr int NKS = D / 16;            // k-steps of Sᵀ = K·Qᵀ
   constexpr int DB = (D + 31) / 32;      // 32-row blocks of Oᵀ
-  constexpr int KP = D + 8;              // K row pitch (elements)
-  constexpr int VP = DB * 32 + 8;        // V row pitch; columns [D, 32 DB) stay zero
+  constexpr int KP = D + 8;              // K row pitch (elements): ds_read_b128 slots 7r, 9r, 13r mod 16 distinct
+  // V row pitch; columns [D, 32 DB) stay zero. The Vᵀ tr16 reads of a 32-lane half cover 4 rows x 16
+  // dwords: a pitch of 16 or 48 dwords mod 64 puts them on 4 disjoint quarters of the bank row (the
+  // round-4 pitch 32 DB + 8 overlapped neighbouring rows: 2-way conflicts)
+  constexpr int VP = DB == 1 ? 32 : DB <= 3 ? 96 : 160;
+  static_assert(VP >= DB * 32 && ((VP / 2) % 64 == 16 || (VP / 2) % 64 == 48), "V pitch");
   constexpr int NCH = D / 8;             // 16-B chunks per key row
   constexpr int NST = (64 * NCH + 255) / 256;  // chunks per thread per tile (K and V each)
   __shared__ __attribute__((aligned(16))) __bf16 Ks[2][64 * KP];

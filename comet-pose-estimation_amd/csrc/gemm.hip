@@ -2727,10 +2727,9 @@ bool dact_ok(const comet_gemm_args& a, int act, const void* pre, int64_t ldpre) 
   if (a.bias || a.resid || a.aux || a.act != COMET_ACT_NONE || a.batch[0] * a.batch[1] != 1) return false;
   if (a.n % 8 != 0 || (uintptr_t)a.c % 16 != 0 || a.ldc % 8 != 0) return false;
   if (pre == nullptr || (uintptr_t)pre % 16 != 0 || ldpre % 8 != 0 || ldpre < a.n) return false;
-  const int bn = big_bn(a);
-  if (bn == 0 || a.k % 64 != 0) return false;
-  const int64_t tiles = cdiv(a.m, big::BM) * cdiv(a.n, bn);
-  return !(tiles < kCUs && a.k / 64 >= 16);  // make_plan would split K: not fused
+  // one predicate with the planner: the fused epilogue exists on the 256-row kernel without split-K
+  const Plan p = make_plan(a);
+  return p.kind == 1 && p.splits == 1 && p.tail == 0 && p.bn == big_bn(a);
 }
 
 template <int BN, int LB>

@@ -1068,7 +1068,7 @@ def test_gemm_small_split_matches_unsplit(la, lb, mnk, out, monkeypatch):
     assert d <= (2 * q + 1e-5) * ref.abs().max().item(), f"split vs unsplit differ by {d:.3e}"
 
 
-# ---- round 4 paths: opt-in COMET_MLP_FUSE=1, the 32-row row-LN tiles (default since round 5); last in the file ----
+# ---- round 4 paths, the defaults since round 5: the fused Mlp node, the 32-row row-LN tiles; last in the file ----
 @pytest.mark.parametrize("M,N2,K2", [(4133, 256, 1024), (8192, 768, 3072)])
 def test_gemm_dact_vs_torch(M, N2, K2):
     """comet_gemm_dact: dPre = GELU'(pre) * (dY @ W) in bf16 and dbias = column sums of the stored
@@ -1097,7 +1097,7 @@ def test_gemm_dact_vs_torch(M, N2, K2):
 
 @pytest.mark.parametrize("rows", [8 * 577, 128])
 def test_mlp_fused_backward_matches_unfused(monkeypatch, rows):
-    """The camera head's Mlp as one autograd node (COMET_MLP_FUSE=1: fc2's input gradient fused with
+    """The camera head's Mlp as one autograd node (the default; fc2's input gradient fused with
     fc1's GELU backward, comet_gemm_dact) against the two-Linear path (GEMM + comet_act_bwd_colsum) at a
     T_P-like shape in bf16: the forward is the same kernels (bit-identical); the gradients differ
     by one bf16 rounding of the hidden gradient (the fused path rounds once). 128 rows (the camera
@@ -1156,3 +1156,30 @@ def test_gemm_rowln_32row_tiles(M, K, monkeypatch):
     v = x.double() @ w.double().t() + b.double() + r.double()
     ln = (v - v.mean(1, keepdim=True)) / torch.sqrt(v.var(1, unbiased=False, keepdim=True) + 1e-6)
     _close(outs[1][0], ln, 1e-4, 1e-4, "rowln 32 vs f64")
+
+
+def test_mlp_narrow_output_takes_two_linear_path():
+    """The GAPR quaternion head's Mlp(768 -> 1536 -> 4) (camera_predictor10.py:385-413): a 4-wide
+    output is not a multiple of 8 (the fused node's column-sum kernels), so mlp() keeps the two
+    Linear nodes; forward and backward run (round 4's COMET_MLP_FUSE=1 raised here in the bench
+    step) and equal the explicit two-Linear path bit for bit."""
+    _ops()
+    from comet_amd import functional as F
+    from comet_amd.models.modules import Mlp
+    torch.manual_seed(1)
+    mlp = Mlp(768, 1536, out_features=4).to(DEV)
+    x0 = torch.randn(128, 768, device=DEV)
+    res = {}
+    for unfused in (False, True):
+        F._MLP_UNFUSED, old = unfused, F._MLP_UNFUSED
+        try:
+            mlp.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            with F.precision(torch.bfloat16):
+                y = mlp(x)
+            y.square().sum().backward()
+        finally:
+            F._MLP_UNFUSED = old
+        res[unfused] = (y.detach(), x.grad, mlp.fc1.weight.grad, mlp.fc2.weight.grad, mlp.fc2.bias.grad)
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
