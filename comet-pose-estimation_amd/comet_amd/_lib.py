@@ -98,6 +98,7 @@ SIGNATURES = {
     "comet_gemm_workspace": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64)]),
     "comet_gemm_plan": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_int32)]),
     "comet_gemm_rowln_ok": (_INT, [ctypes.POINTER(GemmArgs)]),
+    "comet_gemm_rowln_workspace": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(ctypes.c_int64)]),
     "comet_gemm_rowln": (_INT, [ctypes.POINTER(GemmArgs), ctypes.POINTER(RowLNArgs), c_vp]),
     "comet_gemm_dact_ok": (_INT, [ctypes.POINTER(GemmArgs), _INT, c_vp, c_i64]),
     "comet_gemm_dact": (_INT, [ctypes.POINTER(GemmArgs), _INT, c_vp, c_i64, c_vp, c_vp]),

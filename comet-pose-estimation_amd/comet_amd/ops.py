@@ -267,8 +267,15 @@ def linear_rowln(x, w, bias, resid, *, raw=True, y16_eps=None, z=None):
         zw, zb, zeps = z
         z16 = torch.empty(*x.shape[:-1], N, device=x.device, dtype=torch.bfloat16)
         a.z16, a.ldz, a.zw, a.zb, a.eps_z = z16.data_ptr(), N, zw.data_ptr(), zb.data_ptr(), float(zeps)
+    lib = L.load()
+    ws_bytes = ctypes.c_int64(0)
+    L.check(lib.comet_gemm_rowln_workspace(ctypes.byref(g), ctypes.byref(ws_bytes)), "comet_gemm_rowln_workspace")
+    ws = None
+    if ws_bytes.value > 0:  # split-K partials of the few-row path (torch caching allocator)
+        ws = torch.empty((ws_bytes.value + 3) // 4, device=x.device, dtype=torch.float32)
+        g.workspace, g.workspace_bytes = ws.data_ptr(), ws_bytes.value
     e0 = PROF.start()
-    L.check(L.load().comet_gemm_rowln(ctypes.byref(g), ctypes.byref(a), stream()), "comet_gemm_rowln")
+    L.check(lib.comet_gemm_rowln(ctypes.byref(g), ctypes.byref(a), stream()), "comet_gemm_rowln")
     if e0 is not None:
         name = "comet_gemm_rowln"
         if PROF.detail:

@@ -47,6 +47,14 @@ template <> struct AVec<__bf16> { typedef uint4 type; };
 template <> struct AVec<float> { typedef float4 type; };
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// max of two scores without fmaxf's NaN canonicalisation of both operands (two extra v_max_f32 per
+// call on permlane results); the scores are finite or -inf
+__device__ __forceinline__ float vmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 typedef __attribute__((address_space(3))) void lds_void;
 
 template <typename T, int D>
@@ -302,12 +310,17 @@ attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, i
       qf[g][c] = (qrow[g] < lq && d0 < D) ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow[g] * sq_l + d0) : bf16x8{};
     }
   }
-  f32x4 o[QG][DT];
-  float m_run[QG], l_run[QG];
+  // lacc: the row sums of P on the matrix core -- Oᵀ's extra 16-row tile with an all-ones A operand,
+  // so every register of a lane holds its query's sum over the keys so far (the sum of the bf16 P
+  // that the PV MFMAs consume, rescaled with O): 4 MFMAs per tile instead of 16 v_add_f32 per query
+  // group (the kernel is bound by vector issue)
+  f32x4 o[QG][DT], lacc[QG];
+  float m_run[QG];
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, uint4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
 #pragma unroll
   for (int g = 0; g < QG; ++g) {
     m_run[g] = -INFINITY;
-    l_run[g] = 0.f;
+    lacc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < DT; ++i) o[g][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -363,30 +376,30 @@ attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, i
           for (int r = 0; r < 4; ++r)
             if (t * 64 + st * 16 + 4 * hg + r >= lk) s[g][st][r] = -INFINITY;
       }
-      float mt = fmaxf(fmaxf(s[g][0][0], s[g][0][1]), fmaxf(s[g][0][2], s[g][0][3]));
-#pragma unroll
-      for (int st = 1; st < 4; ++st)
-        mt = fmaxf(fmaxf(mt, fmaxf(s[g][st][0], s[g][st][1])), fmaxf(s[g][st][2], s[g][st][3]));
-      mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      // the 16 scores of the lane: a v_max3 tree (8 instructions); the 4 lane groups of a query meet by
+      // v_permlane16_swap / v_permlane32_swap (no LDS round trip as with ds_bpermute)
+      const float* sv = reinterpret_cast<const float*>(&s[g][0]);
+      float mt = fmaxf(fmaxf(fmaxf(sv[0], sv[1]), sv[2]), fmaxf(fmaxf(sv[3], sv[4]), sv[5]));
+      mt = fmaxf(fmaxf(mt, fmaxf(fmaxf(sv[6], sv[7]), sv[8])), fmaxf(fmaxf(sv[9], sv[10]), sv[11]));
+      mt = fmaxf(fmaxf(mt, fmaxf(fmaxf(sv[12], sv[13]), sv[14])), sv[15]);
+      {
+        const auto w16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(mt), __float_as_uint(mt), false, false);
+        mt = vmax_raw(__uint_as_float(w16[0]), __uint_as_float(w16[1]));
+        const auto w32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mt), __float_as_uint(mt), false, false);
+        mt = vmax_raw(__uint_as_float(w32[0]), __uint_as_float(w32[1]));
+      }
       const float m_new = fmaxf(m_run[g], mt * scale_log2);
       if (__ballot(m_new > m_run[g]) != 0) {
         const float alpha = __builtin_amdgcn_exp2f(m_run[g] - m_new);
-        l_run[g] *= alpha;
+        lacc[g] *= alpha;
 #pragma unroll
         for (int i = 0; i < DT; ++i) o[g][i] *= alpha;
         m_run[g] = m_new;
       }
-      float ls = 0.f;
 #pragma unroll
       for (int st = 0; st < 4; ++st)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(s[g][st][r], scale_log2, -m_new));
-          s[g][st][r] = p;
-          ls += p;
-        }
-      l_run[g] += ls;
+        for (int r = 0; r < 4; ++r) s[g][st][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s[g][st][r], scale_log2, -m_new));
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         pf[g][u] = __builtin_shufflevector(__builtin_convertvector(s[g][2 * u], bf16x4),
@@ -404,6 +417,8 @@ attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, i
 #pragma unroll
         for (int g = 0; g < QG; ++g) o[g][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[g][u], o[g][dt], 0, 0, 0);
       }
+#pragma unroll
+      for (int g = 0; g < QG; ++g) lacc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pf[g][u], lacc[g], 0, 0, 0);
     }
   };
 
@@ -424,9 +439,7 @@ attn_fwd_bf16_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, i
 
 #pragma unroll
   for (int g = 0; g < QG; ++g) {
-    float l_tot = l_run[g];
-    l_tot += __shfl_xor(l_tot, 16, 64);
-    l_tot += __shfl_xor(l_tot, 32, 64);
+    const float l_tot = lacc[g][0];
     if (qrow[g] >= lq) continue;
     const float inv = 1.f / l_tot;
     __bf16* orow = O + (int64_t)qrow[g] * so_l;
@@ -500,10 +513,14 @@ attn_fwd32_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
   for (int s = 0; s < NKS; ++s)
     qf[s] = qrow < lq ? *reinterpret_cast<const bf16x8*>(Q + (int64_t)qrow * sq_l + 16 * s + 8 * h) : bf16x8{};
 
-  f32x16 oacc[DB];
+  // lacc: the row sums of P on the matrix core (an all-ones A operand beside the PV MFMAs: every
+  // register of a lane holds its query's sum of the bf16 P consumed so far, rescaled with O), in
+  // place of 32 v_add_f32 per tile
+  f32x16 oacc[DB], lacc = f32x16{};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, uint4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
 #pragma unroll
   for (int i = 0; i < DB; ++i) oacc[i] = f32x16{};
-  float m_run = -INFINITY, l_run = 0.f;
+  float m_run = -INFINITY;
 
   uint4 kst[NST], vst[NST];
   auto gload = [&](int t) {
@@ -554,33 +571,31 @@ attn_fwd32_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
         for (int j = 0; j < 16; ++j)
           if (t * 64 + kb * 32 + (j & 3) + 8 * (j >> 2) + 4 * h >= lk) sacc[kb][j] = -INFINITY;
     }
-    float mt = sacc[0][0];
+    // the lane's 32 scores: a v_max3 tree (16 instructions), then the partner half by permlane32
+    float mt = fmaxf(fmaxf(sacc[0][0], sacc[0][1]), sacc[0][2]);
 #pragma unroll
-    for (int j = 1; j < 16; ++j) mt = fmaxf(mt, sacc[0][j]);
+    for (int j = 3; j < 15; j += 2) mt = fmaxf(fmaxf(mt, sacc[0][j]), sacc[0][j + 1]);
+    mt = fmaxf(fmaxf(mt, sacc[0][15]), sacc[1][0]);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) mt = fmaxf(mt, sacc[1][j]);
+    for (int j = 1; j < 15; j += 2) mt = fmaxf(fmaxf(mt, sacc[1][j]), sacc[1][j + 1]);
+    mt = fmaxf(mt, sacc[1][15]);
     {
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mt), __float_as_uint(mt), false, false);
-      mt = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      mt = vmax_raw(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
     }
     const float m_new = fmaxf(m_run, mt * scale_log2);
     if (__ballot(m_new > m_run) != 0) {  // exact: alpha == 1 for every lane otherwise
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      l_run *= alpha;
+      lacc *= alpha;
 #pragma unroll
       for (int i = 0; i < DB; ++i) oacc[i] *= alpha;
       m_run = m_new;
     }
-    float ls = 0.f;
     bf16x8 pf[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][j], scale_log2, -m_new));
-        sacc[kb][j] = p;
-        ls += p;
-      }
+      for (int j = 0; j < 16; ++j) sacc[kb][j] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[kb][j], scale_log2, -m_new));
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const f32x4 lo = {sacc[kb][8 * s], sacc[kb][8 * s + 1], sacc[kb][8 * s + 2], sacc[kb][8 * s + 3]};
@@ -589,11 +604,11 @@ attn_fwd32_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
                                             0, 1, 2, 3, 4, 5, 6, 7);
       }
     }
-    l_run += ls;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kb][s], lacc, 0, 0, 0);
         const __bf16* va = vs + (kb * 32 + 16 * s) * VP + voff;
 #pragma unroll
         for (int db = 0; db < DB; ++db) {
@@ -617,11 +632,7 @@ attn_fwd32_kernel(const __bf16* __restrict__ Q, int64_t sq_b, int64_t sq_h, int6
   }
   tile(ntiles - 1, (ntiles - 1) & 1, std::true_type{});
 
-  float l_tot = l_run;
-  {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_tot), __float_as_uint(l_tot), false, false);
-    l_tot = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-  }
+  const float l_tot = lacc[0];
   // O rows: lane (r, h) holds d = 32 db + 8u + 4h + (0..3); a v_permlane32_swap per dword of the
   // (u, u + 1) pair gives each lane 8 contiguous d (16-B stores, cdna_hip_programming.md T21)
   const float inv = 1.f / l_tot;

@@ -470,7 +470,7 @@ attn_bwd_dkdv32_kernel(BwdPtrs p) {
     if (tid < 64) {
       const int q = t * 64 + tid;
       lreg = q < p.lq ? LSE[q] * LOG2E_B : INFINITY;  // queries past lq: P = 0
-      dreg = q < p.lq ? DL[q] : 0.f;
+      dreg = q < p.lq ? -DL[q] : 0.f;                 // -Δ: the dPᵀ accumulators start from it
     }
   };
   auto lstore = [&](int buf) {
@@ -491,7 +491,15 @@ attn_bwd_dkdv32_kernel(BwdPtrs p) {
     const __bf16* gs = Gs[buf];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
-      f32x16b sacc = f32x16b{}, pacc = f32x16b{};
+      // register j: query qb*32 + 8(j>>2) + 4h + (j&3); dPᵀ - Δ accumulates onto the -Δ of its query
+      // (one v_mul per score below instead of v_sub + v_mul)
+      f32x16b sacc = f32x16b{}, pacc;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&dl_s[buf][qb * 32 + 8 * u + 4 * h]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pacc[4 * u + e] = d4[e];
+      }
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
         const bf16x8 qa = *reinterpret_cast<const bf16x8*>(qs + (qb * 32 + r) * TP + 16 * s + 8 * h);
@@ -499,16 +507,14 @@ attn_bwd_dkdv32_kernel(BwdPtrs p) {
         sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[s], sacc, 0, 0, 0);
         pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[s], pacc, 0, 0, 0);
       }
-      // register j: query qb*32 + 8(j>>2) + 4h + (j&3)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const f32x4 l4 = *reinterpret_cast<const f32x4*>(&lse_s[buf][qb * 32 + 8 * u + 4 * h]);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(&dl_s[buf][qb * 32 + 8 * u + 4 * h]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float pr = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[4 * u + e], sl2, -l4[e]));
-          sacc[4 * u + e] = pr;                               // P
-          pacc[4 * u + e] = pr * (pacc[4 * u + e] - d4[e]);   // dS (unscaled)
+          sacc[4 * u + e] = pr;                     // P
+          pacc[4 * u + e] = pr * pacc[4 * u + e];   // dS (unscaled)
         }
       }
 #pragma unroll
@@ -606,13 +612,18 @@ attn_bwd_dq32_kernel(BwdPtrs p) {
     }
   };
 
-  auto tile = [&](int t, int buf) {
+  // MASK only for the ragged last key tile (peeled: the per-score key test and select cost ~95 vector
+  // instructions per tile when evaluated on every tile)
+  auto tile = [&](int t, int buf, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
     const __bf16* ks = Ks[buf];
     const __bf16* vs = Vs[buf];
-    const bool ragged = t * 64 + 64 > p.lk;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      f32x16b sacc = f32x16b{}, pacc = f32x16b{};
+      // dPᵀ - Δ accumulates onto -Δ of the lane's query: one v_mul per score below
+      f32x16b sacc = f32x16b{}, pacc;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) pacc[j] = -dl;
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
         const bf16x8 ka = *reinterpret_cast<const bf16x8*>(ks + (kb * 32 + r) * TP + 16 * s + 8 * h);
@@ -624,8 +635,8 @@ attn_bwd_dq32_kernel(BwdPtrs p) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         float pr = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[j], sl2, -lse2));
-        if (ragged && t * 64 + kb * 32 + 8 * (j >> 2) + 4 * h + (j & 3) >= p.lk) pr = 0.f;
-        pacc[j] = pr * (pacc[j] - dl);  // dS (unscaled)
+        if (MASK && t * 64 + kb * 32 + 8 * (j >> 2) + 4 * h + (j & 3) >= p.lk) pr = 0.f;
+        pacc[j] = pr * pacc[j];  // dS (unscaled)
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
@@ -643,12 +654,15 @@ attn_bwd_dq32_kernel(BwdPtrs p) {
   gload(0);
   lstore(0);
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) gload(t + 1);
-    tile(t, t & 1);
-    if (t + 1 < ntiles) lstore((t + 1) & 1);
+  // every tile but the last is full; the last runs the masked instantiation, peeled out of the loop
+  // (one instantiation inside the loop keeps its register allocation that of the unmasked body)
+  for (int t = 0; t < ntiles - 1; ++t) {
+    gload(t + 1);
+    tile(t, t & 1, std::false_type{});
+    lstore((t + 1) & 1);
     __syncthreads();
   }
+  tile(ntiles - 1, (ntiles - 1) & 1, std::true_type{});
   __bf16* dQ = p.dq + b * p.sdq_b + hd * p.sdq_h + (int64_t)qrow * p.sdq_l;
   store_rows32<D>(dQ, qok, acc, p.scale, h);
 }

@@ -1870,9 +1870,112 @@ void pp_tile(const comet_gemm_args& a, int& tbm, int& tbn) {
   }
 }
 
+// Few-row row-LN GEMMs (M <= 32 x CUs: the tracker's 8192 virtual-track tokens) with a long K: the
+// persistent row-LN kernel gives each CU one 32 x 384 tile whose 24 k-tiles of weights (48 KiB each)
+// run behind one load in flight (33.6 us at M 8192 K 1536). Instead: split-K partials of the plain
+// 256-row kernel (raw f32, K / S each, tiles x S ~ one round of CUs), then one reduce that sums the
+// partials in split order, adds bias and residual and writes the LayerNorm outputs, one wave per
+// row (rowln_reduce_kernel). 0 = not taken (COMET_ROWLN_NOSPLIT=1 disables it).
+int rowln_splits(const comet_gemm_args& a) {
+  if ((a.n != 384 && a.n != 256) || getenv("COMET_ROWLN_NOSPLIT") != nullptr) return 0;
+  const int grid = num_cus();
+  if (cdiv(a.m, 32) > grid) return 0;
+  const int64_t tiles = cdiv(a.m, big::BM) * cdiv(a.n, 128), ktiles = a.k / 64;
+  int64_t sp = grid / tiles;
+  if (sp > ktiles / 6) sp = ktiles / 6;  // >= 6 k-tiles per split
+  return sp >= 2 ? (int)sp : 0;
+}
+
+int64_t rowln_ws_bytes(const comet_gemm_args& a, int splits) {
+  return (int64_t)splits * a.m * a.n * (int64_t)sizeof(float);
+}
+
+// One wave per row, N <= 512 and N % 4 == 0: lane l owns columns 4l + 256j. v = alpha * sum of the
+// partials (split order) + bias + beta * resid, then the RowLN outputs (two-pass-free: sum and sum of
+// squares by wave shuffles, var = E[v^2] - mean^2 clamped at 0, as the persistent kernel).
+__global__ void __launch_bounds__(256)
+rowln_reduce_kernel(const float* __restrict__ ws, int splits, int64_t M, int N, const float* __restrict__ bias,
+                    const float* __restrict__ resid, int64_t ldr, float alpha, float beta, float* __restrict__ C,
+                    int64_t ldc, w4::RowLN ln) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[2][4];
+  float s = 0.f, sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = 4 * lane + 256 * j;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[j][e] = 0.f;
+    if (col >= N) continue;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < splits; ++z) {
+      const f32x4 p = *reinterpret_cast<const f32x4*>(ws + ((int64_t)z * M + row) * N + col);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] += p[e];
+    }
+    const f32x4 r = *reinterpret_cast<const f32x4*>(resid + row * ldr + col);
+    f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (bias != nullptr) b = *reinterpret_cast<const f32x4*>(bias + col);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float o = alpha * acc[e] + b[e] + beta * r[e];
+      v[j][e] = o;
+      s += o;
+      sq = fmaf(o, o, sq);
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    s += __shfl_xor(s, m, 64);
+    sq += __shfl_xor(sq, m, 64);
+  }
+  const float invn = 1.f / (float)N;
+  const float mu = s * invn, var = fmaxf(sq * invn - mu * mu, 0.f);
+  const float ry = rsqrtf(var + ln.eps_y), rz = rsqrtf(var + ln.eps_z);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = 4 * lane + 256 * j;
+    if (col >= N) continue;
+    float y[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[e] = (v[j][e] - mu) * ry;
+    *reinterpret_cast<f32x4*>(C + row * ldc + col) =
+        ln.raw_c ? f32x4{v[j][0], v[j][1], v[j][2], v[j][3]} : f32x4{y[0], y[1], y[2], y[3]};
+    if (ln.y16 != nullptr) store4(ln.y16 + row * ln.ldy + col, y);
+    if (ln.z16 != nullptr) {
+      const f32x4 zw = *reinterpret_cast<const f32x4*>(ln.zw + col), zb = *reinterpret_cast<const f32x4*>(ln.zb + col);
+      float z[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) z[e] = (v[j][e] - mu) * rz * zw[e] + zb[e];
+      store4(ln.z16 + row * ln.ldz + col, z);
+    }
+  }
+}
+
+int launch_rowln_split(const comet_gemm_args& a, const w4::RowLN& ln, int splits, hipStream_t s) {
+  Epi e{nullptr, 0, 0, 0, nullptr, 0, 0, 0, 0.f, nullptr, 0, 0, 0, 1.f, COMET_ACT_NONE, 1};
+  const int64_t tiles_m = cdiv(a.m, big::BM), tiles_n = cdiv(a.n, 128);
+  const int64_t kchunk = cdiv(a.k / 64, splits) * 64;
+  splits = (int)cdiv(a.k, kchunk);
+  Split sp{reinterpret_cast<float*>(a.workspace), kchunk};
+  hipLaunchKernelGGL((big::gemm_big_kernel<float, 128, 0, 0, true>), dim3((unsigned)(tiles_m * tiles_n), (unsigned)splits),
+                     dim3(big::NT), 0, s, (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (float*)nullptr, a.ldc,
+                     a.m, a.n, a.k, (int)tiles_n, e, sp);
+  COMET_CHECK_LAUNCH("comet_gemm_rowln (split-K partials)");
+  hipLaunchKernelGGL(rowln_reduce_kernel, dim3((unsigned)cdiv(a.m, 4)), dim3(256), 0, s, sp.ws, splits, a.m, (int)a.n,
+                     a.bias_mode == 1 ? a.bias : nullptr, reinterpret_cast<const float*>(a.resid), a.ldr, a.alpha,
+                     a.beta, reinterpret_cast<float*>(a.c), a.ldc, ln);
+  COMET_CHECK_LAUNCH("comet_gemm_rowln (LN reduce)");
+  return COMET_OK;
+}
+
 // Row-LN launch (comet_gemm_rowln): f32 output with a residual, no activation / aux, one tile
 // spanning the row. Instances: 128 x 384 / 64 x 384 / 32 x 384 (N = 384), 128 x 256 (N = 256).
 int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s) {
+  if (const int sp = rowln_splits(a)) {
+    if (a.workspace != nullptr && a.workspace_bytes >= rowln_ws_bytes(a, sp)) return launch_rowln_split(a, ln, sp, s);
+  }
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, a.alpha, COMET_ACT_NONE, 1};
   e.prio = getenv("COMET_GEMM_PRIO") != nullptr;
   int grid = num_cus();
@@ -2038,6 +2141,10 @@ int choose_splits(const comet_gemm_args& a) {
   const int64_t tiles = cdiv(a.m, BM) * cdiv(a.n, BN) * a.batch[0] * a.batch[1];
   const int bk = a.dtype_ab == COMET_BF16 ? bf::BK : f32::BK;
   const int64_t ktiles = cdiv(a.k, bk);
+  // f32 operands (the f32 camera trunk, T_F: M = 128 tokens) run 16-deep k-tiles, each a global ->
+  // LDS round trip whose latency the tile's 64 MFMAs do not cover: their splits keep >= 2 k-tiles
+  // (bf16: >= 8 of 64) and the weight-gradient shapes (K = 128 tokens, 144 tiles) split too (round 5)
+  const bool f32ab = a.dtype_ab == COMET_F32 && getenv("COMET_GEMM_NO_F32SPLIT") == nullptr;
   if (tiles >= kCUs || ktiles < 16) {
     // few tiles over a short K (the camera trunk's M = 128 token GEMMs: 6 tiles ran 12 serial
     // k-tiles each on 6 CUs): split while every split keeps >= 2 k-tiles (bf16 operands only)
@@ -2047,10 +2154,15 @@ int choose_splits(const comet_gemm_args& a) {
       if (s > 64) s = 64;
       return s < 1 ? 1 : (int)s;
     }
+    if (f32ab && tiles < kCUs && ktiles >= 4) {
+      int64_t s = cdiv(2 * kCUs, tiles);
+      if (s > ktiles / 2) s = ktiles / 2;
+      return s < 1 ? 1 : (int)s;
+    }
     return 1;
   }
   int64_t s = cdiv(2 * kCUs, tiles);
-  const int64_t smax = ktiles / 8;
+  const int64_t smax = f32ab ? ktiles / 2 : ktiles / 8;
   if (s > smax) s = smax;
   if (s > 64) s = 64;
   return s < 1 ? 1 : (int)s;
@@ -2695,6 +2807,18 @@ static bool rowln_ok(const comet_gemm_args& a, const comet_rowln_args* ln) {
   if (!b4(ln->y16, ln->ldy) || !b4(ln->z16, ln->ldz)) return false;
   if (ln->z16 != nullptr && (ln->zw == nullptr || ln->zb == nullptr)) return false;
   return true;
+}
+
+extern "C" int comet_gemm_rowln_workspace(const comet_gemm_args* args, int64_t* bytes) {
+  using namespace comet;
+  COMET_CHECK_ARG(bytes != nullptr, "comet_gemm_rowln_workspace: null bytes");
+  *bytes = 0;
+  const int rc = validate(args);
+  if (rc != COMET_OK) return rc;
+  if (rowln_ok(*args, nullptr)) {
+    if (const int sp = rowln_splits(*args)) *bytes = rowln_ws_bytes(*args, sp);
+  }
+  return COMET_OK;
 }
 
 extern "C" int comet_gemm_rowln_ok(const comet_gemm_args* args) {

@@ -104,6 +104,10 @@ typedef struct comet_rowln_args {
   int32_t raw_c;
 } comet_rowln_args;
 int comet_gemm_rowln_ok(const comet_gemm_args* args);
+/* Few rows (M <= 32 x CUs) and a long K: the row-LN GEMM runs as split-K partials + one LN reduce when
+ * args->workspace holds comet_gemm_rowln_workspace() bytes (0: no split; without the workspace the
+ * single-kernel path runs, same outputs within f32 summation order). */
+int comet_gemm_rowln_workspace(const comet_gemm_args* args, int64_t* bytes);
 int comet_gemm_rowln(const comet_gemm_args* args, const comet_rowln_args* ln, void* stream);
 
 /* GEMM + activation backward (Mlp.fc2's input gradient fused with fc1's GELU backward and bias

@@ -486,6 +486,24 @@ def test_act_bwd_colsum(act, dtypes):
            f"act_bwd_colsum db act={act}")
 
 
+@pytest.mark.parametrize("rows,cols", [(0, 768), (1, 4), (5, 100), (128, 768), (128, 3072), (577, 768),
+                                       (4096, 392), (4097, 392), (20000, 130)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_colsum(rows, cols, dtype):
+    """comet_colsum (the f32 path's bias gradients) vs f64 sums, on a strided (ld > cols) view, both
+    without and with accumulate: the few-rows kernel (rows <= 4096, round 5) and the atomic one."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(rows + cols)
+    big = torch.randn(rows, cols + 24, generator=g).to(dtype).to(DEV)
+    x = big[:, 8:8 + cols]
+    ref = x.double().sum(0)
+    out = ops.colsum(x)
+    _close(out, ref, 1e-5, 1e-5 * max(1.0, math.sqrt(rows)), f"colsum {rows}x{cols} {dtype}")
+    acc = torch.full((cols,), 2.5, device=DEV)
+    ops.colsum(x, out=acc, accumulate=True)
+    _close(acc, ref + 2.5, 1e-5, 1e-5 * max(1.0, math.sqrt(rows)), f"colsum accumulate {rows}x{cols} {dtype}")
+
+
 @pytest.mark.parametrize("D", [32, 48, 64, 96])
 @pytest.mark.parametrize("lq,lk", [(577, 577), (130, 1000), (16, 16), (200, 70)])
 def test_flash_attention_bwd(D, lq, lk):
@@ -1144,6 +1162,7 @@ def test_gemm_rowln_32row_tiles(M, K, monkeypatch):
     b = _rand(N, seed=123, scale=0.1).to(DEV)
     r = _rand(M, N, seed=124).to(DEV)
     zw, zb = (1 + _rand(N, seed=125, scale=0.1)).to(DEV), _rand(N, seed=126, scale=0.1).to(DEV)
+    monkeypatch.setenv("COMET_ROWLN_NOSPLIT", "1")  # the persistent kernel's tiles, not the split-K path
     outs = []
     for v32 in (False, True):
         if v32:
@@ -1183,3 +1202,39 @@ def test_mlp_narrow_output_takes_two_linear_path():
         res[unfused] = (y.detach(), x.grad, mlp.fc1.weight.grad, mlp.fc2.weight.grad, mlp.fc2.bias.grad)
     for a, b in zip(res[False], res[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M,N,K,raw,zed", [(8192, 384, 1536, False, True), (8192, 384, 1536, False, False),
+                                           (8192 - 40, 384, 1536, True, False), (4096 + 8, 256, 1024, False, True),
+                                           (8192, 384, 768, True, True)])
+def test_gemm_rowln_split_reduce(M, N, K, raw, zed, monkeypatch):
+    """Few-row row-LN GEMMs with a long K (round 5: split-K partials of the 256-row kernel + one LN
+    reduce, comet_gemm_rowln_workspace > 0) equal the single-kernel persistent path
+    (COMET_ROWLN_NOSPLIT=1) within f32 summation order, and the f64 LayerNorm; row tails, N = 256."""
+    ops = _ops()
+    from comet_amd import _lib as L
+    import ctypes
+    x = _rand(M, K, seed=131).to(torch.bfloat16).to(DEV)
+    w = _rand(N, K, seed=132, scale=K ** -0.5).to(torch.bfloat16).to(DEV)
+    b = _rand(N, seed=133, scale=0.1).to(DEV)
+    r = _rand(M, N, seed=134).to(DEV)
+    z = ((1 + _rand(N, seed=135, scale=0.1)).to(DEV), _rand(N, seed=136, scale=0.1).to(DEV), 1e-5) if zed else None
+    g = ops._rowln_args(x, w, r, b, r)
+    nb = ctypes.c_int64(0)
+    L.check(L.load().comet_gemm_rowln_workspace(ctypes.byref(g), ctypes.byref(nb)), "ws")
+    assert nb.value > 0, "the split path must be taken at this shape"
+    outs = []
+    for nosplit in (False, True):
+        if nosplit:
+            monkeypatch.setenv("COMET_ROWLN_NOSPLIT", "1")
+        outs.append(ops.linear_rowln(x, w, b, r, raw=raw, y16_eps=1e-6, z=z))
+    monkeypatch.delenv("COMET_ROWLN_NOSPLIT")
+    for a, c, what in zip(outs[0], outs[1], ("c", "y16", "z16")):
+        if c is None:
+            assert a is None
+            continue
+        tol = 2e-5 if what == "c" else 8e-3
+        _close(a, c.double(), tol, tol, f"rowln split vs single {what} M{M} N{N} K{K}")
+    v = x.double() @ w.double().t() + b.double() + r.double()
+    ln = (v - v.mean(1, keepdim=True)) / torch.sqrt(v.var(1, unbiased=False, keepdim=True) + 1e-6)
+    _close(outs[0][0], v if raw else ln, 1e-4, 1e-4, "rowln split vs f64")
