@@ -179,32 +179,89 @@ class Stats:
 
 # ------------------------------------------------------------------------------------------------
 class _BatchShard(torch.utils.data.Sampler):
-    """Batch i of the wrapped batch sampler goes to rank i % world (accelerate's default batch
-    dispatch, split_batches=False); the tail that does not fill every rank is dropped so all
-    ranks run the same number of steps."""
+    """Batch i of the wrapped batch sampler goes to rank i % world: accelerate's BatchSamplerShard
+    without split_batches (accelerate==0.24.0, requirements.txt:1; installed by train_e2epose2.py:83's
+    accelerator.prepare), restated here:
+
+      * every rank yields batches only once all ranks have a full one (a round of `world` batches);
+      * drop_last=True on the wrapped sampler: the last incomplete round is dropped;
+      * even_batches=True (accelerate's default): the last round is completed -- and a short last
+        batch filled -- with indices cycled from the start of the epoch (the first `world` batches),
+        so every rank runs the same number of steps on full batches;
+      * even_batches=False (abl_ours.py:28): the last round's batches go to the first ranks as they
+        are, so the last ranks may run one batch fewer.
+    `batch_size` / `drop_last` are read from the wrapped sampler (a plain list of batches: batch size
+    None -- variable-length batches, cycled whole -- and drop_last False), as accelerate does.
+    Pinned against the installed accelerate's implementation of the same algorithm
+    (tests/test_checkpoint_cpu.py::test_batch_shard_matches_accelerate)."""
 
     def __init__(self, batch_sampler, rank, world, even_batches=True):
         self.bs, self.rank, self.world, self.even = batch_sampler, rank, world, even_batches
+        self.batch_size = getattr(batch_sampler, "batch_size", None)
+        self.drop_last = getattr(batch_sampler, "drop_last", False)
 
     def __len__(self):
         n = len(self.bs)
-        if self.even:
+        if n % self.world == 0:
             return n // self.world
-        return n // self.world + (1 if self.rank < n % self.world else 0)
+        length = n // self.world
+        if self.drop_last:
+            return length
+        if self.even:
+            return length + 1
+        return length + 1 if self.rank < n % self.world else length
 
     def __iter__(self):
-        n = len(self.bs) // self.world if self.even else None
-        for i, b in enumerate(self.bs):
-            if n is not None and i // self.world >= n:
-                break
-            if i % self.world == self.rank:
-                yield b
+        W, R, bsz = self.world, self.rank, self.batch_size
+        initial = []       # the first W batches' indices (flat), or the batches themselves (bsz None)
+        pending = None     # this rank's batch of the current round, yielded once the round is full
+        idx, batch = -1, []
+        for idx, batch in enumerate(self.bs):
+            if not self.drop_last and idx < W:
+                if bsz is None:
+                    initial.append(batch)
+                else:
+                    initial += list(batch)
+            if idx % W == R:
+                pending = batch
+            if idx % W == W - 1 and (bsz is None or len(batch) == bsz):
+                yield pending
+                pending = None
+        if self.drop_last or not initial:
+            return
+        if not self.even:
+            if pending:
+                yield pending
+            return
+        if pending and (bsz is None or len(pending) == bsz):
+            yield pending
+        need = W * bsz if bsz is not None else W
+        while len(initial) < need:  # datasets smaller than one round
+            initial += initial
+        if bsz is None or len(batch) == bsz:  # the last batch seen was full (and yielded by its rank)
+            batch = []
+            idx += 1
+        batch = list(batch)
+        cyc = 0
+        while idx % W != 0 or len(batch) > 0:
+            if bsz is None:
+                batch = initial[cyc]
+                cyc += 1
+            else:
+                end = cyc + bsz - len(batch)
+                batch = batch + initial[cyc:end]
+                cyc = end
+            if idx % W == R:
+                yield batch
+            batch = []
+            idx += 1
 
 
 class CometAccelerator:
-    """even_batches=False (abl_ours.py:28): the batches that do not fill every rank are kept, so
-    the last ranks may run one batch fewer, instead of being dropped (this build never pads by
-    repeating samples, so even_batches=True drops that tail)."""
+    """accelerate.Accelerator subset of the reference's loops. Batches shard over ranks as
+    accelerate's BatchSamplerShard does (_BatchShard): even_batches=True (train_e2epose2.py) completes
+    the last round with samples cycled from the epoch's start; even_batches=False (abl_ours.py:28)
+    keeps the batches that do not fill every rank, so the last ranks may run one batch fewer."""
 
     def __init__(self, mixed_precision="no", device=None, bucket_mb=25, even_batches=True):
         import torch.distributed as dist

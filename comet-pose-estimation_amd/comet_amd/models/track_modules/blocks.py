@@ -185,5 +185,14 @@ class EfficientUpdateFormer(nn.Module):
 
 
 def _flow(tokens, init, head):
-    x = ops.add(tokens.contiguous(), init)
+    """flow_head(tokens + init) (blocks.py:347). Without gradients in bf16 compute (the frozen
+    tracker) the sum is written straight in bf16, one rounding of the f32 sum as the reference's f32
+    add + autocast cast (one pass instead of an f32 add and a cast)."""
+    tokens = tokens.contiguous()
+    if (F.compute_dtype() == torch.bfloat16 and not torch.is_grad_enabled() and init.dtype == torch.float32
+            and init.is_contiguous() and init.shape == tokens.shape):
+        C = tokens.shape[-1]
+        x = ops.add_rows(tokens, init.reshape(-1, C), period=tokens.numel() // C, out_dtype=torch.bfloat16)
+        return F.linear(x, head.weight, head.bias, out_dtype=torch.float32)
+    x = ops.add(tokens, init)
     return F.linear(x, head.weight, head.bias, out_dtype=torch.float32)

@@ -46,6 +46,21 @@ __global__ void add_rows_kernel(const TI* __restrict__ x, const float* __restric
   }
 }
 
+// y = x + t elementwise (t f32, same shape), 4 elements per thread-step: the update formers' flow-head
+// input (blocks.py:347, tokens + init) written straight in the GEMM's bf16 (one rounding of the f32 sum,
+// as the reference's f32 add followed by autocast's cast)
+template <typename TI, typename TO>
+__global__ void add_cast4_kernel(const TI* __restrict__ x, const float* __restrict__ t, TO* __restrict__ y, int64_t n4) {
+  GRID_STRIDE(i, n4) {
+    float a[4], b[4];
+    loadn<4>(x + 4 * i, a);
+    loadn<4>(t + 4 * i, b);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) a[e] += b[e];
+    storen<4>(y + 4 * i, a);
+  }
+}
+
 template <typename T>
 __global__ void rowscale_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w, T* __restrict__ y,
                                     int64_t rows, int64_t cols) {
@@ -367,6 +382,18 @@ extern "C" int comet_add_rows(int dtype_x, int dtype_y, const void* x, const flo
   COMET_CHECK_ARG(x && table && y && period > 0, "comet_add_rows: bad args");
   if (rows == 0) return COMET_OK;
   hipStream_t s = as_stream(stream);
+  const int64_t n = rows * cols;
+  if (period >= rows && ldx == cols && ldy == cols && n % 4 == 0 &&
+      ((uintptr_t)x | (uintptr_t)table | (uintptr_t)y) % 16 == 0) {  // plain elementwise: vector path
+#define AC(TI, TO) hipLaunchKernelGGL((add_cast4_kernel<TI, TO>), dim3(g1d(n / 4)), dim3(256), 0, s, (const TI*)x, table, (TO*)y, n / 4)
+    if (dtype_x == COMET_F32 && dtype_y == COMET_F32) AC(float, float);
+    else if (dtype_x == COMET_F32 && dtype_y == COMET_BF16) AC(float, __bf16);
+    else if (dtype_x == COMET_BF16 && dtype_y == COMET_F32) AC(__bf16, float);
+    else AC(__bf16, __bf16);
+#undef AC
+    COMET_CHECK_LAUNCH("comet_add_rows (elementwise)");
+    return COMET_OK;
+  }
   const unsigned g = g1d(rows * cols);
 #define AR(TI, TO) hipLaunchKernelGGL((add_rows_kernel<TI, TO>), dim3(g), dim3(256), 0, s, (const TI*)x, table, (TO*)y, rows, cols, period, ldx, ldy)
   if (dtype_x == COMET_F32 && dtype_y == COMET_F32) AR(float, float);

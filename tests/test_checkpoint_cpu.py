@@ -223,12 +223,44 @@ def test_process_spark_data2_defaults():
 
 
 def test_batch_shard_partitions_batches():
+    """drop_last=True on the wrapped sampler: 11 batches over 4 ranks -> the incomplete last round
+    (3 batches) is dropped, every rank runs 2 full batches, all distinct."""
     from comet_amd.loop import _BatchShard
-    bs = list(torch.utils.data.BatchSampler(range(23), batch_size=2, drop_last=True))  # 11 batches
+    bs = torch.utils.data.BatchSampler(range(23), batch_size=2, drop_last=True)  # 11 batches
     shards = [list(_BatchShard(bs, r, 4)) for r in range(4)]
     assert all(len(s) == len(_BatchShard(bs, 0, 4)) == 2 for s in shards)
     flat = [tuple(b) for s in shards for b in s]
     assert len(set(flat)) == 8 and set(flat) <= {tuple(b) for b in bs}
+
+
+def test_batch_shard_even_batches_cycles_from_start():
+    """even_batches=True, drop_last=False (accelerate's default, train_e2epose2.py): 23 samples in
+    batches of 2 (the last one short) over 4 ranks -> 3 full batches per rank; the short batch is
+    completed and the round filled with indices cycled from the start of the epoch."""
+    from comet_amd.loop import _BatchShard
+    bs = torch.utils.data.BatchSampler(range(23), batch_size=2, drop_last=False)  # 12 batches, last [22]
+    shards = [list(_BatchShard(bs, r, 4)) for r in range(4)]
+    assert [len(s) for s in shards] == [3, 3, 3, 3] == [len(_BatchShard(bs, r, 4)) for r in range(4)]
+    assert all(len(b) == 2 for s in shards for b in s)
+    assert shards[3][2] == [22, 0]  # the short last batch completed from index 0
+    assert sorted(i for s in shards for b in s for i in b) == sorted(list(range(23)) + [0])
+
+
+@pytest.mark.parametrize("n,bsz,world,drop_last,even", [
+    (23, 2, 4, False, True), (23, 2, 4, False, False), (23, 2, 4, True, True), (24, 2, 4, False, True),
+    (5, 1, 2, False, True), (5, 1, 2, False, False), (3, 4, 4, False, True), (7, 3, 2, False, True),
+    (100, 8, 8, False, True), (100, 8, 8, True, True), (1, 2, 3, False, True), (9, 2, 8, False, False)])
+def test_batch_shard_matches_accelerate(n, bsz, world, drop_last, even):
+    """_BatchShard restates accelerate's BatchSamplerShard (split_batches=False): the same batches on
+    every rank, in order, and the same lengths, against the installed accelerate (the reference pins
+    0.24.0; the algorithm for a fixed batch size is unchanged since)."""
+    acc = pytest.importorskip("accelerate.data_loader")
+    from comet_amd.loop import _BatchShard
+    bs = torch.utils.data.BatchSampler(range(n), batch_size=bsz, drop_last=drop_last)
+    for r in range(world):
+        ours, ref = _BatchShard(bs, r, world, even), acc.BatchSamplerShard(bs, world, r, False, even)
+        assert [list(b) for b in ours] == [list(b) for b in ref], (r, list(ours), list(ref))
+        assert len(ours) == len(ref)
 
 
 def test_batch_shard_uneven_keeps_tail():

@@ -1238,3 +1238,19 @@ def test_gemm_rowln_split_reduce(M, N, K, raw, zed, monkeypatch):
     v = x.double() @ w.double().t() + b.double() + r.double()
     ln = (v - v.mean(1, keepdim=True)) / torch.sqrt(v.var(1, unbiased=False, keepdim=True) + 1e-6)
     _close(outs[0][0], v if raw else ln, 1e-4, 1e-4, "rowln split vs f64")
+
+
+@pytest.mark.parametrize("dt_in,dt_out", [(torch.float32, torch.bfloat16), (torch.float32, torch.float32),
+                                          (torch.bfloat16, torch.float32)])
+@pytest.mark.parametrize("rows,cols", [(4096 * 16, 384), (3, 4), (5, 6)])
+def test_add_rows_elementwise(dt_in, dt_out, rows, cols):
+    """comet_add_rows with period == rows (the update formers' tokens + init before the flow head,
+    round 5: the 4-wide elementwise path when aligned, the generic path otherwise) equals torch's f32
+    sum rounded once to the output dtype."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(rows + cols)
+    x = torch.randn(rows, cols, generator=g).to(dt_in).to(DEV)
+    t = torch.randn(rows, cols, generator=g).to(DEV)
+    y = ops.add_rows(x, t, period=rows, out_dtype=dt_out)
+    ref = (x.float() + t).to(dt_out)
+    assert y.dtype == dt_out and torch.equal(y, ref)
