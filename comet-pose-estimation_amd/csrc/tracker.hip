@@ -394,6 +394,53 @@ tokens_rows_kernel(const float* __restrict__ coords, const float* __restrict__ f
   }
 }
 
+// One wave per token row, 4 consecutive columns per lane step (tdim % 4 == 0): the row's flow,
+// frame-0 row and position row resolved once per wave, 8-B (bf16) / 16-B (f32) stores instead of the
+// row-blocked kernel's 2-B ones (its 664-column rows also left 90 of 256 threads idle per block)
+template <typename TO>
+__global__ void __launch_bounds__(256)
+tokens_wave4_kernel(const float* __restrict__ coords, const float* __restrict__ feats, int latent,
+                    const float* __restrict__ corr, int64_t ldcorr, int corrdim,
+                    const float* __restrict__ pos, int tdim, TO* __restrict__ x, int64_t rows, int S) {
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const int E = latent / 2, c_corr = 2 * E + 2, c_feat = c_corr + corrdim, c_pad = c_feat + latent;
+  const int64_t bn = t / S, t0 = bn * S;
+  const float fx = coords[t * 2] - coords[t0 * 2];
+  const float fy = coords[t * 2 + 1] - coords[t0 * 2 + 1];
+  const float* prow = pos + bn * tdim;
+  const float* crow = corr + t * ldcorr;
+  const float* frow = feats + t * latent;
+  TO* xrow = x + t * tdim;
+  const float dscale = 1000.0f / (float)E;
+  for (int c0 = 4 * lane; c0 < tdim; c0 += 256) {
+    float v[4];
+    loadn<4>(prow + c0, v);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c0 + e;
+      float u;
+      if (c < 2 * E) {
+        const float a = c < E ? fx : fy;
+        const int cc = c < E ? c : c - E;
+        const float arg = a * ((float)(cc & ~1) * dscale);
+        u = (cc & 1) ? cosf(arg) : sinf(arg);
+      } else if (c < c_corr) {
+        u = c == 2 * E ? fx : fy;
+      } else if (c < c_feat) {
+        u = crow[c - c_corr];
+      } else if (c < c_pad) {
+        u = frow[c - c_feat];
+      } else {
+        u = 0.f;
+      }
+      v[e] += u;
+    }
+    storen<4>(xrow + c0, v);
+  }
+}
+
 // coords[t] += delta[t, 0:2] for s > 0 (frame 0 pinned, base_track_predictor.py:247-254);
 // preds[it][b, s, n] = coords * scale (layout [B, S, N, 2]).
 template <typename TD>
@@ -793,7 +840,14 @@ extern "C" int comet_tracker_tokens(int dtype_out, const float* coords, const fl
   COMET_CHECK_ARG(coords && feats && corr && pos && x && tdim >= latent * 2 + 2 + corrdim, "comet_tracker_tokens: bad args");
   if (rows == 0) return COMET_OK;
   hipStream_t s = as_stream(stream);
-  if (rows < (1ll << 31) && S > 0 && getenv("COMET_TOKENS_FLAT") == nullptr) {
+  const bool al = ((uintptr_t)x % (dtype_out == COMET_F32 ? 16 : 8)) == 0 && (uintptr_t)pos % 16 == 0;
+  if (tdim % 4 == 0 && al && S > 0 && getenv("COMET_TOKENS_ROWS") == nullptr && getenv("COMET_TOKENS_FLAT") == nullptr) {
+    const unsigned gr = (unsigned)cdiv(rows, 4);
+    if (dtype_out == COMET_F32)
+      hipLaunchKernelGGL((tokens_wave4_kernel<float>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (float*)x, rows, S);
+    else
+      hipLaunchKernelGGL((tokens_wave4_kernel<__bf16>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (__bf16*)x, rows, S);
+  } else if (rows < (1ll << 31) && S > 0 && getenv("COMET_TOKENS_FLAT") == nullptr) {
     const RowBlock rb = make_rowblock(rows, tdim);
     const unsigned gr = (unsigned)cdiv(rb.nrows, rb.RB);
     if (dtype_out == COMET_F32)

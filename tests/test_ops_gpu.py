@@ -741,8 +741,9 @@ def test_layernorm_persistent_rows(cols, xdt, ydt, monkeypatch):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_tracker_tokens_row_blocked(dtype, monkeypatch):
-    """comet_tracker_tokens (base_track_predictor.py:186-222 token assembly): row-blocked kernel
-    bit-identical to the flat element-wise kernel, incl. the zero pad columns."""
+    """comet_tracker_tokens (base_track_predictor.py:186-222 token assembly): the wave-per-row
+    4-column kernel (default, round 5) and the row-blocked kernel (COMET_TOKENS_ROWS=1) bit-identical
+    to the flat element-wise kernel, incl. the zero pad columns."""
     ops = _ops()
     B, N, S, lat, corrdim = 2, 37, 5, 128, 324
     tdim = 2 * (lat // 2) + 2 + corrdim + lat + 6
@@ -753,10 +754,13 @@ def test_tracker_tokens_row_blocked(dtype, monkeypatch):
     pos = _rand(B * N, tdim, seed=133).to(DEV)
     x1 = torch.empty(rows, tdim, device=DEV, dtype=dtype)
     x2 = torch.empty(rows, tdim, device=DEV, dtype=dtype)
+    x3 = torch.empty(rows, tdim, device=DEV, dtype=dtype)
     ops.tracker_tokens(coords, feats, lat, corr, corrdim, pos, tdim, x1, rows, S)
+    monkeypatch.setenv("COMET_TOKENS_ROWS", "1")
+    ops.tracker_tokens(coords, feats, lat, corr, corrdim, pos, tdim, x3, rows, S)
     monkeypatch.setenv("COMET_TOKENS_FLAT", "1")
     ops.tracker_tokens(coords, feats, lat, corr, corrdim, pos, tdim, x2, rows, S)
-    assert torch.equal(x1, x2)
+    assert torch.equal(x1, x2) and torch.equal(x3, x2)
     # spot check against the definition: frame-0 rows have zero flow -> emb = sin(0)/cos(0)
     E = lat // 2
     r0 = x1[0].float().cpu() - pos[0].cpu()

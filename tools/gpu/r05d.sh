@@ -11,7 +11,7 @@ export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
 O=gpurun_out/$TAG
 mkdir -p $O
 step() { echo "== $*" >&2; "$@" || { echo "step failed ($?): $*"; exit 1; }; }
-step timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_ops_gpu.py -k "attention or attn or colsum or mlp or rowln or gemm or add_rows" > $O/tests.log 2>&1
+step timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_ops_gpu.py -k "attention or attn or colsum or mlp or rowln or gemm or add_rows or tokens" > $O/tests.log 2>&1
 tail -2 $O/tests.log
 for r in 1 2; do
   for lib in libcomet_hip.so libcomet_hip_attnA.so; do
