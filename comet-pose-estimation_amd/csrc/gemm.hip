@@ -2141,10 +2141,6 @@ int choose_splits(const comet_gemm_args& a) {
   const int64_t tiles = cdiv(a.m, BM) * cdiv(a.n, BN) * a.batch[0] * a.batch[1];
   const int bk = a.dtype_ab == COMET_BF16 ? bf::BK : f32::BK;
   const int64_t ktiles = cdiv(a.k, bk);
-  // f32 operands (the f32 camera trunk, T_F: M = 128 tokens) run 16-deep k-tiles, each a global ->
-  // LDS round trip whose latency the tile's 64 MFMAs do not cover: their splits keep >= 2 k-tiles
-  // (bf16: >= 8 of 64) and the weight-gradient shapes (K = 128 tokens, 144 tiles) split too (round 5)
-  const bool f32ab = a.dtype_ab == COMET_F32 && getenv("COMET_GEMM_NO_F32SPLIT") == nullptr;
   if (tiles >= kCUs || ktiles < 16) {
     // few tiles over a short K (the camera trunk's M = 128 token GEMMs: 6 tiles ran 12 serial
     // k-tiles each on 6 CUs): split while every split keeps >= 2 k-tiles (bf16 operands only)
@@ -2154,15 +2150,10 @@ int choose_splits(const comet_gemm_args& a) {
       if (s > 64) s = 64;
       return s < 1 ? 1 : (int)s;
     }
-    if (f32ab && tiles < kCUs && ktiles >= 4) {
-      int64_t s = cdiv(2 * kCUs, tiles);
-      if (s > ktiles / 2) s = ktiles / 2;
-      return s < 1 ? 1 : (int)s;
-    }
     return 1;
   }
   int64_t s = cdiv(2 * kCUs, tiles);
-  const int64_t smax = f32ab ? ktiles / 2 : ktiles / 8;
+  const int64_t smax = ktiles / 8;
   if (s > smax) s = smax;
   if (s > 64) s = 64;
   return s < 1 ? 1 : (int)s;
