@@ -181,6 +181,13 @@ def _rank(rank, world, port, q, paths, size):
         local = {k: p.grad.detach().cpu().numpy().copy() for k, p in model.camera_predictor.named_parameters()
                  if p.grad is not None and k in SELECT}
         model.zero_grad(set_to_none=True)
+        # and once more: the step is run-to-run deterministic (up to the f32 atomics of bias / norm
+        # weight gradients), also with the other rank's kernels interleaved on the same device
+        fwd_bwd()
+        torch.cuda.synchronize()
+        again = {k: float(np.abs(p.grad.detach().cpu().numpy() - local[k]).max() / max(np.abs(local[k]).max(), 1e-30))
+                 for k, p in model.camera_predictor.named_parameters() if p.grad is not None and k in SELECT}
+        model.zero_grad(set_to_none=True)
         bk = GradBucketer(model.camera_predictor.parameters(), bucket_mb=25)
         res = []
         for step in range(2):  # step 0 = bucket discovery, step 1 = rebuilt buckets with overlap
@@ -198,11 +205,11 @@ def _rank(rank, world, port, q, paths, size):
         during = all(d for _, d in bk.launch_log)
         print(f"{size} rank {rank}: B={br}, {len(bk.buckets)} buckets, peak device memory "
               f"{torch.cuda.max_memory_allocated() / 2**30:.1f} GiB", flush=True)
-        q.put((rank, res, g, during, len(bk.buckets), local))
+        q.put((rank, res, g, during, len(bk.buckets), local, again))
         dist.destroy_process_group()
     except Exception as e:  # surface the error to the parent
         import traceback
-        q.put((rank, None, traceback.format_exc(), None, None, None))
+        q.put((rank, None, traceback.format_exc(), None, None, None, None))
         raise
 
 
@@ -221,19 +228,23 @@ def test_ddp_simulated_ranks_equal_B2_gradients(size):
         p.start()
     got = {}
     for _ in range(2):
-        rank, res, g, during, nb, local = q.get(timeout=600)
+        rank, res, g, during, nb, local, again = q.get(timeout=600)
         assert res is not None, g
         got[rank] = (res, g, during, nb, local)
+        for k, v in again.items():
+            print(f"{size} rank {rank} {k}: second local pass vs first rel-to-max {v:.2e}")
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     # (a) the exchange: reduced == mean of the local gradients
+    errs = []
     for rank in (0, 1):
         for k, v in got[rank][1].items():
             mean = (got[0][4][k].astype(np.float64) + got[1][4][k].astype(np.float64)) / 2
             err = np.abs(v - mean).max() / max(np.abs(mean).max(), 1e-30)
             print(f"{size} rank {rank} {k}: reduced vs mean(local) rel-to-max {err:.2e}")
-            assert err < 1e-5, (rank, k, err)
+            errs.append((err, rank, k))
+    assert max(errs)[0] < 1e-5, max(errs)
     # (b) single process, B = 2
     seed, T, S, N, dtype, _ = SIZES[size]
     model, cfg = _model()
