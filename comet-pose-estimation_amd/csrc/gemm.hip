@@ -1021,21 +1021,6 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int SG_MFMA = 0x008, SG_DSR = 0x100, SG_VMR = 0x020;
 
-// One LDS-DMA piece (16 B per lane, 1 KiB per wave at the wave-uniform LDS address l). Variant build
-// COMET_GEMM_ASM_DMA issues it from inline asm: hipcc then no longer sees the LDS writes and drops
-// the vmcnt(0) it inserts before the first ds_read of every k-step 0 (its alias analysis cannot tell
-// the slot being read from the slot the DMA of k-tile q+2 is filling), which cut the DMA's landing
-// time from ~2 k-steps to ~1. The kernel's own counted waits and barriers already order every DMA
-// before its readers, and it drains vmcnt before exit (an LDS write must not outlive the wave).
-__device__ __forceinline__ void glds16(const void* g, lds_void* l) {
-#ifdef COMET_GEMM_ASM_DMA
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)l);
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" :: "s"(la), "v"(g) : "m0");
-#else
-  __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
-#endif
-}
-
 #ifdef COMET_GEMM_STAMPS
 // Diagnostic build only (make STAMPS=1 -> libcomet_hip_stamp.so): wave 0 of each workgroup records
 // the shader clock at the start of each tile's k-loop (0), before (1) and after (2) its epilogue,
@@ -1189,13 +1174,14 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     const __bf16* pa = ldA + la_kt * BK;
 #pragma unroll
     for (int p = 0; p < PA; ++p)
-      glds16((const void*)(pa + offA[p]), (lds_void*)(smem + slot * ASTAGE + (pieca + p) * 512));
+      __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + slot * ASTAGE + (pieca + p) * 512), 16, 0, 0);
   };
   auto issue_b = [&](int slot) {
     const __bf16* pb = ldB + lb_kt * BK;
 #pragma unroll
     for (int p = 0; p < PB; ++p)
-      glds16((const void*)(pb + offB[p]), (lds_void*)(smem + BRING + slot * BSTAGE + (wid * PB + p) * 512));
+      __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]),
+                                       (lds_void*)(smem + BRING + slot * BSTAGE + (wid * PB + p) * 512), 16, 0, 0);
   };
   // one batch: A and B pieces interleaved (lockstep), or all B pieces before the A pieces (AR)
   auto issue_cur = [&](int aslot, int bslot) {
@@ -1208,9 +1194,10 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 #pragma unroll
       for (int p = 0; p < (PA > PB ? PA : PB); ++p) {
         if (p < PA)
-          glds16((const void*)(pa + offA[p]), (lds_void*)(smem + aslot * ASTAGE + (pieca + p) * 512));
+          __builtin_amdgcn_global_load_lds((const void*)(pa + offA[p]), (lds_void*)(smem + aslot * ASTAGE + (pieca + p) * 512), 16, 0, 0);
         if (p < PB)
-          glds16((const void*)(pb + offB[p]), (lds_void*)(smem + BRING + bslot * BSTAGE + (wid * PB + p) * 512));
+          __builtin_amdgcn_global_load_lds((const void*)(pb + offB[p]),
+                                           (lds_void*)(smem + BRING + bslot * BSTAGE + (wid * PB + p) * 512), 16, 0, 0);
       }
     }
   };
@@ -1811,8 +1798,6 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 #ifdef COMET_GEMM_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   COMET_STAMP(my_tiles, 3);
-#elif defined(COMET_GEMM_ASM_DMA)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stream's trailing re-loads land before exit
 #endif
 }
 }  // namespace w4
