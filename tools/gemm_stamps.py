@@ -4,10 +4,11 @@
         python tools/gemm_stamps.py M N K [act] [f32|bf16] [resid]
 
 (make -C comet-pose-estimation_amd STAMPS=1 builds the library.) Wave 0 of each workgroup stamps
-the shader clock at each tile's k-loop start (0), before (1) and after (2) its epilogue, and at the
-end after draining its stores (3). Prints, over the workgroups, the k-loop cycles per tile, the
-epilogue cycles per tile, the gap from one tile's epilogue end to the next tile's k-loop start, the
-first k-loop start (from the earliest workgroup start) and the store drain at the end.
+the shader clock at each tile's k-loop start (0), before (1) and after (2) its epilogue; waves 0 and 4
+(one SIMD's pair) stamp k-tile 3 of each tile: its start, k-step 0 issued, past the waits, past the
+barrier, k-step 1 issued. Prints, over the workgroups, the k-loop and epilogue cycles per tile, the
+gap between tiles and the k-tile-3 segments per wave. Only 256 x 256 instances keep their counted
+vmcnt waits exact with the stamp stores in the loop (the A-ring instances leave pieces in flight).
 """
 import ctypes
 import os
@@ -60,39 +61,37 @@ def main():
     st = buf.reshape(WG, TILES, 8).astype(np.int64)
     used = st[:, 0, 0] != 0
     st = st[used]
-    kl, ep, gap, ends, kf, p1, bw, k0, k1s, k1w = [], [], [], [], [], [], [], [], [], []
-    ntile = []
+    kl, ep, gap, ntile = [], [], [], []
+    # intra-k-tile stamps of k-tile 3 (waves 0 and 4: tile slots t and t + 32): 3 k-tile start,
+    # 4 k-step 0 issued, 5 past the waits, 6 past the barrier, 7 k-step 1 issued
+    seg = {w: {"k-step 0 issue": [], "waits": [], "barrier": [], "k-step 1 issue": [], "k-tile": []} for w in (0, 4)}
     for w_ in st:
-        n = int(np.count_nonzero(w_[:, 0]))
+        n = min(int(np.count_nonzero(w_[:32, 0])), 32)
         ntile.append(n)
         for t in range(n):
             kl.append(w_[t, 1] - w_[t, 0])
-            kf.append(w_[t, 3] - w_[t, 0])
-            if w_[t, 6] and w_[t, 7]:  # k-tile 0 past its barrier (6); k-tile 1 before its wait (7)
-                k0.append(w_[t, 6] - w_[t, 0])
-                k1s.append(w_[t, 7] - w_[t, 6])
-                k1w.append(w_[t, 3] - w_[t, 7])
             ep.append(w_[t, 2] - w_[t, 1])
-            if w_[t, 4]:  # row-LN epilogue: pass 1 end (4), statistics barrier passed (5)
-                p1.append(w_[t, 4] - w_[t, 1])
-                bw.append(w_[t, 5] - w_[t, 4])
             if t + 1 < n:
                 gap.append(w_[t + 1, 0] - w_[t, 2])
-        ends.append(w_[n, 3] - w_[n - 1, 2] if n < TILES and w_[n, 3] else 0)  # tile n: only the end stamp
+            for w, row in ((0, w_[t]), (4, w_[t + 32])):
+                if all(row[i] for i in (3, 4, 5, 6, 7)):
+                    d = seg[w]
+                    d["k-step 0 issue"].append(row[4] - row[3])
+                    d["waits"].append(row[5] - row[4])
+                    d["barrier"].append(row[6] - row[5])
+                    d["k-step 1 issue"].append(row[7] - row[6])
+                    d["k-tile"].append(row[7] - row[3])
     f = lambda a: f"mean {np.mean(a):8.0f}  p10 {np.percentile(a, 10):8.0f}  p90 {np.percentile(a, 90):8.0f}"  # noqa: E731
     nk = K // 64  # (s_memtime counters are per XCD: only differences within a workgroup are used)
     print(f"M{M} N{N} K{K} {('rowln ' + ln_mode) if ln_mode else f'act{act}'} {odt} res{int(res)}: {us:.1f} us, {2 * M * N * K / us / 1e6:.0f} TF/s; "
-          f"{len(st)} workgroups, tiles per workgroup {min(ntile)}-{max(ntile)}, {nk} k-tiles per tile")
+          f"{len(st)} workgroups, tiles per workgroup (first 32) {min(ntile)}-{max(ntile)}, {nk} k-tiles per tile")
     print(f"  k-loop per tile   (cycles) {f(kl)}   per k-tile {np.mean(kl) / nk:.0f}")
-    print(f"  k-loop to the 2nd k-tile's barrier (cycles) {f(kf)}; rest per k-tile {(np.mean(kl) - np.mean(kf)) / max(nk - 1, 1):.0f}")
-    if k0:
-        print(f"  k-tile 0 to its barrier passed {f(k0)}; k-step 1 + k-tile 1's k-step 0 {f(k1s)}; "
-              f"k-tile 1's wait + barrier {f(k1w)}")
+    for w in (0, 4):
+        for k, v in seg[w].items():
+            if v:
+                print(f"  k-tile 3, wave {w}: {k:15s} {f(v)}")
     print(f"  epilogue per tile (cycles) {f(ep)}")
-    if p1:
-        print(f"  row-LN pass 1 {f(p1)}; statistics barrier {f(bw)}")
     print(f"  gap to next tile  (cycles) {f(gap) if gap else '-'}")
-    print(f"  store drain at end (cycles) {f(ends)}")
     print(f"  share: k-loop {np.sum(kl) / (np.sum(kl) + np.sum(ep) + np.sum(gap)):.3f}  "
           f"epilogue {np.sum(ep) / (np.sum(kl) + np.sum(ep) + np.sum(gap)):.3f}")
 

@@ -10,7 +10,9 @@ export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
 O=gpurun_out/$TAG
 mkdir -p $O
 step() { echo "== $*" >&2; "$@" || { echo "step failed ($?): $*"; exit 1; }; }
-step timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1
+rc=$?; echo "gpu tests rc $rc"
+[ $rc -le 1 ] || { echo "GPU suite ended abnormally ($rc): stopping"; exit 1; }  # 1 = test failures only
 tail -2 $O/gpu_tests.log
 step bash tools/gpu/measure.sh $TAG/m
 step bash tools/gpu/pmc.sh $TAG/pmc
