@@ -42,6 +42,9 @@ class GradBucketer:
         # a backward outside prepare_backward / finish_backward raises unless `local` is set (the
         # bench's timing pass without the exchange): an unreduced gradient would let ranks diverge
         self.local = False
+        # tests: keep a copy of every bucket as it was just before its all-reduce (pre_reduce[bi])
+        self.record = False
+        self.pre_reduce = {}
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
     # ---------------------------------------------------------------------------------------
@@ -103,6 +106,11 @@ class GradBucketer:
         bi, off = self.slot[p]
         return self.flat[bi][off:off + p.numel()].view_as(p)
 
+    def pre_reduce_grad(self, p):
+        """This rank's gradient of p as its bucket held it before the all-reduce (record=True)."""
+        bi, off = self.slot[p]
+        return self.pre_reduce[bi][off:off + p.numel()].view_as(p)
+
     # ---------------------------------------------------------------------------------------
     def prepare_backward(self):
         for buf in self.flat:
@@ -123,6 +131,8 @@ class GradBucketer:
             return
         self.launched[bi] = True
         self.launch_log.append((bi, self.in_backward))
+        if self.record:  # enqueued before the collective, which waits for this stream's work
+            self.pre_reduce[bi] = self.flat[bi].clone()
         if self.world == 1:
             return
         op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM

@@ -1033,9 +1033,21 @@ __device__ __forceinline__ void stamp(int bid, int wid, int tile, int ph) {
   if (wid == 0 && bid < ST_WG && tile < ST_TILES && (threadIdx.x & 63) == 0)
     g_stamps[((bid * ST_TILES + tile) << 3) + ph + (threadIdx.x & 63)] = t;
 }
+// intra-k-tile stamps of waves 0 and 4 (the two waves of one SIMD) on k-tile 3 of tiles 0..31:
+// wave 4 records into tile slot + 32 (phases 3: k-tile start, 4: k-step 0 issued, 5: past the
+// waits, 6: past the barrier, 7: k-step 1 issued; tools/gemm_stamps.py ksteps)
+__device__ __forceinline__ void kstamp(int bid, int wid, int tile, int ph) {
+  __builtin_amdgcn_sched_barrier(0);
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  if ((wid == 0 || wid == 4) && bid < ST_WG && tile < 32 && (threadIdx.x & 63) == 0)
+    g_stamps[((bid * ST_TILES + tile + (wid == 4 ? 32 : 0)) << 3) + ph] = t;
+  __builtin_amdgcn_sched_barrier(0);
+}
 #define COMET_STAMP(tile, ph) stamp(bid, wid, (tile), (ph))
+#define COMET_KSTAMP(tile, ph) kstamp(bid, wid, (tile), (ph))
 #else
 #define COMET_STAMP(tile, ph) ((void)0)
+#define COMET_KSTAMP(tile, ph) ((void)0)
 #endif
 
 // Row LayerNorm fused into the f32 epilogue when one tile spans the whole output row (N == TBN:
@@ -1051,7 +1063,7 @@ struct RowLN {
   int raw_c;
 };
 
-template <typename TC, int ACT, bool HASR, int NW, int TBM, int TBN, bool LN = false>
+template <typename TC, int ACT, bool HASR, int NW, int TBM, int TBN, bool LN = false, bool PING = false>
 __global__ void __launch_bounds__(NW * 64, 1)
 gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restrict__ B, int64_t ldb,
                TC* __restrict__ C, int64_t ldc, int64_t M, int64_t N, int64_t K, int tiles_n, int ntiles,
@@ -1243,8 +1255,575 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 
   // static priority for the younger half of the workgroup (cdna_hip_programming.md T5, static
   // form): the second-dispatched waves lose VALU / issue arbitration on every segment otherwise
-  if (epi.prio && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  if (!PING && epi.prio && wid >= NW / 2) __builtin_amdgcn_s_setprio(1);
   int pend = 0;  // 1: the last epilogue's stores are the newest VMEM ops (count known)
+  // epilogue of tile tix (q_: its last k-tile, qa1_: the A slot of k-tile q_ + 1, for the re-read of
+  // the next tile's first fragments the lock-step loop needs after it)
+  auto tile_epilogue = [&](const int tix, const int q_, const int qa1_) {
+      COMET_STAMP(tix, 1);
+      // ---- epilogue of the tile, straight from the accumulators: lane (li, g) of fragment
+      // (i, j) holds C[row0 + i*16 + li][col0 + j*16 + 4g + r], r = 0..3
+      int tm, tn;
+      tile_rc(off + tix * G, tiles_m, tiles_n, tm, tn);
+      const int64_t row0 = (int64_t)tm * TBM + wr * WROWS + li;
+      const int64_t col0 = (int64_t)tn * TBN + wc * WCOLS + 4 * g;
+      const TC* R = reinterpret_cast<const TC*>(epi.resid);
+      TC* X = reinterpret_cast<TC*>(epi.aux);
+      const bool interior = (int64_t)tm * TBM + TBM <= M && (int64_t)tn * TBN + TBN <= N;
+      // loads first (bias, the first residual row), then a store stream with no wait in it: the
+      // residual rows are prefetched one ahead, so their waits only cover the previous row's stores.
+      // Interior tiles take a branch-free copy (no per-store exec branches, whose joins make the
+      // compiler drain every outstanding store before each block).
+      auto epilogue = [&](auto edge_t) {
+        constexpr bool EDGE = decltype(edge_t)::value;
+        const bool bias_c = epi.bias != nullptr;  // per-column bias only (pp_ok)
+        float bc[NI][4];
+  #pragma unroll
+        for (int j = 0; j < NI; ++j)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) bc[j][r] = 0.f;
+        if (bias_c) {  // one uniform branch around straight-line loads (clamped: tail columns never stored)
+  #pragma unroll
+          for (int j = 0; j < NI; ++j)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int64_t col = col0 + j * 16 + r;
+              bc[j][r] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
+            }
+        }
+        float rc[NI][4], rn[NI][4];
+        auto load_resid = [&](int i, float (&rv)[NI][4]) {
+          const int64_t row = row0 + i * 16;
+  #pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int64_t col = col0 + j * 16;
+            if (!EDGE || (row < M && col < N)) load4(R + row * epi.ldr + col, rv[j]);
+          }
+        };
+        if constexpr (HASR) load_resid(0, rc);
+  #pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          if constexpr (HASR) {
+            if (i + 1 < MI) load_resid(i + 1, rn);
+          }
+          const int64_t row = row0 + i * 16;
+  #pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int64_t col = col0 + j * 16;
+            if (!EDGE || (row < M && col < N)) {
+              float v[4];
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = epi.alpha * acc[i][j][r] + bc[j][r];
+              if (X) store4(X + row * epi.ldaux + col, v);
+              apply_act_n<4>(ACT, v);
+              if constexpr (HASR) {
+  #pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += epi.beta * rc[j][r];
+              }
+              store4(C + row * ldc + col, v);
+            }
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          if constexpr (HASR) {
+  #pragma unroll
+            for (int j = 0; j < NI; ++j)
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) rc[j][r] = rn[j][r];
+          }
+        }
+      };
+      if constexpr (LN) {
+        // row-LN epilogue (tiles_n == 1, N == TBN). Pass 1 is the parked pass of the plain f32
+        // epilogue; each lane's final values (8 lanes x NV columns of one row per wave) go back into
+        // the accumulator registers they were parked from, and the lane's row sum and sum of squares
+        // are reduced over the 8 lanes of the row, then over the WN waves of the tile row through
+        // the LDS table st (one barrier; var = E[v^2] - mean^2, clamped at 0). Pass 2 writes the
+        // outputs with the statistics read back per row (no per-row arrays in registers).
+        constexpr int CPL = 4, NTC = WCOLS / (8 * CPL), NV = NTC * CPL;
+        float* park = reinterpret_cast<float*>(smem + RING) + wid * 8 * PPITCH;
+        float* st = reinterpret_cast<float*>(smem + RING + 2 * PARK_F);
+        const int rr = lane >> 3, cc = lane & 7;
+        const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;  // + i*16 + h*8
+        // (tn is always 0 here; keeping it in the column makes the bias / affine loads tile-dependent
+        // so they are not hoisted out of the k-loop, where they would hold ~36 registers)
+        const int pc0 = tn * TBN + wc * WCOLS + cc * CPL;  // + t*8*CPL + e
+        const float invn = 1.f / (float)N;
+        auto VK = [&](int i, int h, int u) -> float { return acc[i][h * NTC + (u >> 2)][u & 3]; };
+        auto lrow = [&](int i, int h) { return (wr * WROWS + i * 16 + h * 8 + rr) * WN; };
+        auto red8 = [](float x) {
+          x += __shfl_xor(x, 1, 64);
+          x += __shfl_xor(x, 2, 64);
+          x += __shfl_xor(x, 4, 64);
+          return x;
+        };
+        // (mean, biased variance) of row (i, h) from the WN (sum, sum of squares) partials
+        auto rowstats = [&](int i, int h, float& mu, float& var) {
+          float x = 0.f, q = 0.f;
+  #pragma unroll
+          for (int w = 0; w < WN; ++w) {
+            const float2 p = *reinterpret_cast<const float2*>(st + 2 * (lrow(i, h) + w));
+            x += p.x;
+            q += p.y;
+          }
+          mu = x * invn;
+          var = fmaxf(q * invn - mu * mu, 0.f);
+        };
+        auto lnepilogue = [&](auto edge_t) {
+          constexpr bool EDGE = decltype(edge_t)::value;
+          float bcp[NV];
+  #pragma unroll
+          for (int u = 0; u < NV; ++u) bcp[u] = 0.f;
+          if (epi.bias != nullptr) {
+  #pragma unroll
+            for (int t = 0; t < NTC; ++t) load4(epi.bias + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(bcp + t * CPL));
+          }
+          // residual rows are loaded one (i, h) step ahead (a 2-slot register ring), so each step's HBM
+          // latency overlaps the previous step's park / reduce / store work instead of being exposed
+          // MI x 2 times (a 3-slot ring measured 4 % slower on the 64 x 384 tiles; round 4: every residual
+          // row of a 64 x 384 tile issued at once, and a 4-slot ring on the 128-row tiles, 1-6 % slower,
+          // profiles/r04_rowln)
+          constexpr int RDL = 2;
+          auto rload = [&](int ih, float (&dst)[NTC][CPL]) {
+            const int64_t row = prow0 + (ih >> 1) * 16 + (ih & 1) * 8;
+  #pragma unroll
+            for (int t = 0; t < NTC; ++t)
+  #pragma unroll
+              for (int e = 0; e < CPL; ++e) dst[t][e] = 0.f;
+            if constexpr (HASR) {
+  #pragma unroll
+              for (int t = 0; t < NTC; ++t)
+                if (!EDGE || row < M) loadn<CPL>(R + row * epi.ldr + pc0 + t * 8 * CPL, dst[t]);
+            }
+          };
+          float rring[RDL][NTC][CPL];
+  #pragma unroll
+          for (int d = 0; d < RDL - 1; ++d) rload(d, rring[d]);
+  #pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            float vh[2][NV];
+  #pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int64_t row = prow0 + i * 16 + h * 8;
+              const bool live = !EDGE || row < M;
+              const int ih = 2 * i + h;
+              float (&rc)[NTC][CPL] = rring[ih % RDL];
+              if (ih + RDL - 1 < 2 * MI) rload(ih + RDL - 1, rring[(ih + RDL - 1) % RDL]);
+              if ((li >> 3) == h) {
+  #pragma unroll
+                for (int j = 0; j < NI; ++j)
+                  *reinterpret_cast<f32x4*>(park + (li & 7) * PPITCH + (((j * 4 + g) ^ pswz(li & 7)) << 2)) = acc[i][j];
+              }
+              asm volatile("" ::: "memory");
+              float s = 0.f, sq = 0.f;
+  #pragma unroll
+              for (int t = 0; t < NTC; ++t) {
+                float v[CPL];
+                const int lc = (t * 8 * CPL + cc * CPL) >> 2;
+                const f32x4 p4 = *reinterpret_cast<const f32x4*>(park + rr * PPITCH + ((lc ^ pswz(rr)) << 2));
+                v[0] = p4[0]; v[1] = p4[1]; v[2] = p4[2]; v[3] = p4[3];
+  #pragma unroll
+                for (int e = 0; e < CPL; ++e) {
+                  float o = apply_act(ACT, epi.alpha * v[e] + bcp[t * CPL + e]);
+                  if constexpr (HASR) o += epi.beta * rc[t][e];
+                  v[e] = o;
+                  vh[h][t * CPL + e] = o;
+                  s += o;
+                  sq = fmaf(o, o, sq);
+                }
+                if (ln.raw_c && live) storen<CPL>(C + row * ldc + pc0 + t * 8 * CPL, v);
+              }
+              s = red8(s);
+              sq = red8(sq);
+              if (cc == 0) *reinterpret_cast<float2*>(st + 2 * (lrow(i, h) + wc)) = float2{s, sq};
+              asm volatile("" ::: "memory");
+            }
+  #pragma unroll
+            for (int h = 0; h < 2; ++h)
+  #pragma unroll
+              for (int t = 0; t < NTC; ++t)
+                acc[i][h * NTC + t] = f32x4{vh[h][4 * t], vh[h][4 * t + 1], vh[h][4 * t + 2], vh[h][4 * t + 3]};
+          }
+          float zw[NV], zb[NV];
+          if (ln.z16 != nullptr) {
+  #pragma unroll
+            for (int t = 0; t < NTC; ++t) {
+              load4(ln.zw + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(zw + t * CPL));
+              load4(ln.zb + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(zb + t * CPL));
+            }
+          }
+          COMET_STAMP(tix, 4);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          COMET_STAMP(tix, 5);
+          // pass 2: outputs, row by row (mean / rstd once per row, affine weights loaded before the
+          // barrier: a load issued after this epilogue's stores would wait for them)
+  #pragma unroll
+          for (int i = 0; i < MI; ++i)
+  #pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int64_t row = prow0 + i * 16 + h * 8;
+              if (EDGE && row >= M) continue;
+              float mu, var;
+              rowstats(i, h, mu, var);
+              const float ry = rsqrtf(var + ln.eps_y), rz = rsqrtf(var + ln.eps_z);
+  #pragma unroll
+              for (int t = 0; t < NTC; ++t) {
+                const int col = pc0 + t * 8 * CPL;
+                float y[CPL];
+  #pragma unroll
+                for (int e = 0; e < CPL; ++e) y[e] = (VK(i, h, t * CPL + e) - mu) * ry;
+                if (!ln.raw_c) storen<CPL>(C + row * ldc + col, y);
+                if (ln.y16 != nullptr) store4(ln.y16 + row * ln.ldy + col, y);
+                if (ln.z16 != nullptr) {
+                  float z[CPL];
+  #pragma unroll
+                  for (int e = 0; e < CPL; ++e)
+                    z[e] = (VK(i, h, t * CPL + e) - mu) * rz * zw[t * CPL + e] + zb[t * CPL + e];
+                  store4(ln.z16 + row * ln.ldz + col, z);
+                }
+              }
+            }
+  #pragma unroll
+          for (int i = 0; i < MI; ++i)
+  #pragma unroll
+            for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        };
+        if (interior) lnepilogue(std::false_type{});
+        else lnepilogue(std::true_type{});
+        // the next tile's k-step-0 fragments again (buffer (q+1)&1 still holds k-tile q+1): the
+        // copies read during k-step 1 are dead here, so their registers serve the epilogue
+        if constexpr (!PING) read_frags(qa1_, (q_ + 1) & 1, 0, a0, b0);
+      } else if (BPARK && interior && epi.bpark) {
+        if constexpr (BPARK) {
+          __bf16* slab0 = smem + RING + wid * 2 * BSLAB;
+          const int rr = lane >> 3, cc = lane & 7;
+          float bc[NI][4];
+  #pragma unroll
+          for (int j = 0; j < NI; ++j)
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) bc[j][e] = 0.f;
+          if (epi.bias != nullptr) {  // one uniform branch around straight-line loads
+  #pragma unroll
+            for (int j = 0; j < NI; ++j)
+  #pragma unroll
+              for (int e = 0; e < 4; ++e) bc[j][e] = epi.bias[col0 + j * 16 + e];
+          }
+          // per-lane output bases: rows srow0 + i*16 + h*8 (the block offsets are uniform)
+          const int64_t srow0 = (int64_t)tm * TBM + wr * WROWS + rr;
+          const int64_t scol = (int64_t)tn * TBN + wc * WCOLS + cc * 8;
+          TC* cbase = C + srow0 * ldc + scol;
+          // slab layout: row r (0..15) of the block, 16-B chunk k stored at chunk k ^ (r & 7), and the
+          // two 8-B halves of a chunk swapped for rows 8..15 (the fragment writes -- rows li and li + 8
+          // in one lane group -- then hit distinct banks; the row reads are conflict-free)
+          const int wofs = li * WCOLS + ((g & 1) ^ (li >> 3)) * 4;
+          const int rofs = rr * WCOLS + ((cc ^ rr) << 3);
+          // PRE: the activation is applied before parking (no pre-activation copy); otherwise the parked
+          // pre-activation is stored to X and the activation applied to the re-read values. Two
+          // straight-line bodies: a per-element branch on X splits the GELU chains into basic blocks.
+          auto body = [&](auto pre_t) {
+            constexpr bool PRE = decltype(pre_t)::value;
+            TC* xbase = PRE ? nullptr : X + srow0 * epi.ldaux + scol;
+  #pragma unroll
+            for (int i = 0; i < MI; ++i) {
+              __bf16* slab = slab0 + (i & 1) * BSLAB;
+  #pragma unroll
+              for (int j = 0; j < NI; ++j) {
+                float v[4];
+  #pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  v[e] = epi.alpha * acc[i][j][e] + bc[j][e];
+                  if constexpr (PRE) v[e] = apply_act(ACT, v[e]);
+                }
+                *reinterpret_cast<uint2*>(slab + wofs + (((2 * j + (g >> 1)) ^ (li & 7)) << 3)) =
+                    uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+                acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+              }
+              asm volatile("" ::: "memory");
+  #pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                uint4 d = *reinterpret_cast<const uint4*>(slab + h * 8 * WCOLS + rofs);
+                if (h == 1) d = uint4{d.z, d.w, d.x, d.y};
+                const int64_t roff = (int64_t)(i * 16 + h * 8);
+                if constexpr (!PRE) {
+                  *reinterpret_cast<uint4*>(xbase + roff * epi.ldaux) = d;
+                  const unsigned u[4] = {d.x, d.y, d.z, d.w};
+                  unsigned o[4];
+  #pragma unroll
+                  for (int e = 0; e < 4; ++e)
+                    o[e] = pack_bf16x2(apply_act(ACT, bf16_lo(u[e])), apply_act(ACT, bf16_hi(u[e])));
+                  d = uint4{o[0], o[1], o[2], o[3]};
+                }
+                *reinterpret_cast<uint4*>(cbase + roff * ldc) = d;
+              }
+              asm volatile("" ::: "memory");
+            }
+          };
+          if (X == nullptr) body(std::true_type{});
+          else body(std::false_type{});
+          if constexpr (!PING) read_frags(qa1_, (q_ + 1) & 1, 0, a0, b0);
+        }
+      } else if constexpr (BPARK) {
+        epilogue(std::true_type{});  // edge tiles (or unaligned outputs): masked direct stores
+      } else if constexpr (PARK) {
+        // parked epilogue: per 8-row half of each 16-row block the wave parks its 8 x WCOLS raw
+        // accumulators in its own LDS slab (no barrier: only this wave touches it) and re-reads them
+        // row-contiguously, so every store / residual load instruction covers 8 rows x 128 B
+        constexpr int CPL = 16 / (int)sizeof(TC);       // output columns per lane per access (16 B)
+        constexpr int NTC = WCOLS / (8 * CPL);          // column passes per row
+        float* park = reinterpret_cast<float*>(smem + RING) + wid * 8 * PPITCH;
+        const int rr = lane >> 3, cc = lane & 7;
+        const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;        // + i*16 + h*8
+        const int64_t pcol0 = (int64_t)tn * TBN + wc * WCOLS + cc * CPL;  // + t*8*CPL
+        auto pepilogue = [&](auto edge_t) {
+          constexpr bool EDGE = decltype(edge_t)::value;
+          const bool bias_c = epi.bias != nullptr;  // per-column bias only (pp_ok)
+          float bcp[NTC][CPL];
+  #pragma unroll
+          for (int t = 0; t < NTC; ++t)
+  #pragma unroll
+            for (int e = 0; e < CPL; ++e) bcp[t][e] = 0.f;
+          if (bias_c) {
+  #pragma unroll
+            for (int t = 0; t < NTC; ++t)
+  #pragma unroll
+              for (int e = 0; e < CPL; ++e) {
+                const int64_t col = pcol0 + t * 8 * CPL + e;
+                bcp[t][e] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
+              }
+          }
+          // residual rows prefetched RD (i, h) steps ahead into a register ring (the next tile's
+          // k-step-0 fragments are re-read after the epilogue, so their registers hold the ring):
+          // each step's residual load then has RD - 1 steps of park / store work to land in (3 steps:
+          // epilogue 39.5k -> 32.1k cycles per 256 x 256 f32 tile, K 3072 GEMM 835 -> 900 TF/s)
+          constexpr int NSTEP = 2 * MI, RD = HASR ? 4 : 1;
+          float rq[RD][NTC][CPL];
+          auto rld = [&](int st, float (&dst)[NTC][CPL]) {
+            const int64_t row = prow0 + (st >> 1) * 16 + (st & 1) * 8;
+  #pragma unroll
+            for (int t = 0; t < NTC; ++t) {
+              const int64_t col = pcol0 + t * 8 * CPL;
+              if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, dst[t]);
+            }
+          };
+          if constexpr (HASR) {
+  #pragma unroll
+            for (int d = 0; d < RD; ++d)
+              if (d < NSTEP) rld(d, rq[d]);
+          }
+  #pragma unroll
+          for (int i = 0; i < MI; ++i)
+  #pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              float (&rc)[NTC][CPL] = rq[(2 * i + h) % RD];
+              const int64_t row = prow0 + i * 16 + h * 8;
+              if ((li >> 3) == h) {
+  #pragma unroll
+                for (int j = 0; j < NI; ++j)
+                  *reinterpret_cast<f32x4*>(park + (li & 7) * PPITCH + (((j * 4 + g) ^ pswz(li & 7)) << 2)) = acc[i][j];
+              }
+              asm volatile("" ::: "memory");
+  #pragma unroll
+              for (int t = 0; t < NTC; ++t) {
+                const int64_t col = pcol0 + t * 8 * CPL;
+                float v[CPL];
+  #pragma unroll
+                for (int e = 0; e < CPL; e += 4) {
+                  const int lc = (t * 8 * CPL + cc * CPL + e) >> 2;
+                  const f32x4 p4 = *reinterpret_cast<const f32x4*>(park + rr * PPITCH + ((lc ^ pswz(rr)) << 2));
+                  v[e] = p4[0]; v[e + 1] = p4[1]; v[e + 2] = p4[2]; v[e + 3] = p4[3];
+                }
+                if (!EDGE || (row < M && col < N)) {
+  #pragma unroll
+                  for (int e = 0; e < CPL; ++e) v[e] = epi.alpha * v[e] + bcp[t][e];
+                  if (X) storen<CPL>(X + row * epi.ldaux + col, v);
+                  apply_act_n<CPL>(ACT, v);
+                  if constexpr (HASR) {
+  #pragma unroll
+                    for (int e = 0; e < CPL; ++e) v[e] += epi.beta * rc[t][e];
+                  }
+                  storen<CPL>(C + row * ldc + col, v);
+                }
+              }
+              if constexpr (HASR) {
+                if (2 * i + h + RD < NSTEP) rld(2 * i + h + RD, rc);
+              }
+              asm volatile("" ::: "memory");
+              if (h == 1) {
+  #pragma unroll
+                for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+              }
+            }
+        };
+        if (interior) pepilogue(std::false_type{});
+        else pepilogue(std::true_type{});
+        if constexpr (HASR) if constexpr (!PING) read_frags(qa1_, (q_ + 1) & 1, 0, a0, b0);
+      } else {
+      if constexpr (WIDE) {
+        if (interior && X == nullptr && epi.wide) {
+          // lane (li, g) of fragment (i, j) holds row li, columns 16j + 4g .. +3 (bf16-packed as uint2);
+          // permlane16_swap(frag j, frag j+1) exchanges 16-lane groups 1 <-> 0 and 3 <-> 2, after which
+          // group g holds 8 contiguous columns: 16(j + (g & 1)) + 8(g >> 1) .. +7
+          const bool bias_c = epi.bias != nullptr;
+          float bc[NI][4];
+  #pragma unroll
+          for (int j = 0; j < NI; ++j)
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) bc[j][e] = bias_c ? epi.bias[col0 + j * 16 + e] : 0.f;
+          const int64_t wcol = (int64_t)tn * TBN + wc * WCOLS + 16 * (g & 1) + 8 * (g >> 1);
+  #pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int64_t row = row0 + i * 16;
+  #pragma unroll
+            for (int j = 0; j < NI; j += 2) {
+              unsigned pk[2][2];
+  #pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                float v[4];
+  #pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = epi.alpha * acc[i][j + u][e] + bc[j + u][e];
+                apply_act_n<4>(ACT, v);
+                pk[u][0] = pack_bf16x2(v[0], v[1]);
+                pk[u][1] = pack_bf16x2(v[2], v[3]);
+                acc[i][j + u] = f32x4{0.f, 0.f, 0.f, 0.f};
+              }
+              const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+              const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+              *reinterpret_cast<uint4*>(C + row * ldc + wcol + 16 * j) = uint4{s0[0], s1[0], s0[1], s1[1]};
+            }
+          }
+        } else if (interior) {
+          epilogue(std::false_type{});
+        } else {
+          epilogue(std::true_type{});
+        }
+      } else {
+      if (interior) epilogue(std::false_type{});
+      else epilogue(std::true_type{});
+      }
+      }
+      // interior: every VMEM op this epilogue issued came after the LDS-DMA of k-tile q+2 and their
+      // count is fixed, so the next barrier wait leaves them in flight
+      if (BPARK && interior && epi.bpark) pend = X != nullptr ? 3 : 2;
+      else if constexpr (WIDE) pend = (interior && X == nullptr && epi.wide) ? 1 : 0;
+      else pend = interior ? 1 : 0;
+      COMET_STAMP(tix, 2);
+  };
+  if constexpr (PING) {
+    // ---- ping-pong k-loop (256 x 256 tiles; PING instances): 32-deep k-steps through a 4-slot ring
+    // of [A 256 x 32 | B 256 x 32] images (the 128 KiB of the lock-step ring). Waves 4-7 run one
+    // barrier behind waves 0-3, and each k-step of a wave is a memory segment (its 12 fragments of
+    // this k-step, its LDS-DMA pieces of k-step p + 3, the waits) and an MFMA segment (32 MFMAs at
+    // raised priority), each closed by a barrier: one group's MFMAs always run beside the other
+    // group's reads, DMA issue and barrier waits, where the lock-step loop had both SIMD partners
+    // waiting at once (profiles/r05_l: ~1.2k of ~4k cycles per k-tile with the MFMA pipe idle).
+    // Fragments are single-buffered (read in the segment that precedes their MFMAs).
+    // Hazards (p = global k-step, slot p % 4): the DMA of k-step p + 3 refills the slot of k-step
+    // p - 1, whose last reads (group 1's, retired by lgkmcnt(0) before its first barrier of k-step
+    // p - 1, which is group 0's second) precede every wave's memory segment of k-step p; the
+    // pieces of k-step p + 1 are retired (vmcnt: the two younger k-steps' 8 pieces stay in flight)
+    // before the first barrier of k-step p, two barriers before any read of them.
+    constexpr int KSA = TBM * 32, KSL = (TBM + TBN) * 32;  // bf16 elements: A image, one slot
+    static_assert(TBM == 256 && TBN == 256 && NW == 8 && !LN, "ping-pong k-loop: 256 x 256 tiles, 8 waves");
+    static_assert(4 * KSL <= RING, "ping-pong ring");
+    const int nks = (int)(K / 32);
+    const int P = my_tiles * nks;
+    const int grp = wid >> 2;
+    // one LDS-DMA piece = 16 rows x 32 k: lane -> row lane >> 2 of the piece, LDS chunk lane & 3
+    // holding source chunk (lane & 3) ^ ((row >> 1) & 3); per wave and k-step pieces 2 wid, 2 wid + 1
+    // of the A image and of the B image (rows clamped: tail rows re-read the last row, never stored)
+    int s_it = 0, s_ks = 0;
+    const __bf16* sA = A;
+    const __bf16* sB = B;
+    int oA[2], oB[2];
+    auto pset = [&](int it) {
+      int tm, tn;
+      tile_rc(off + it * G, tiles_m, tiles_n, tm, tn);
+      const int m0 = tm * TBM, n0 = tn * TBN;
+      sA = A + (int64_t)m0 * lda;
+      sB = B + (int64_t)n0 * ldb;
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int r = (wid * 2 + pp) * 16 + (lane >> 2);
+        const int sw = ((lane & 3) ^ ((r >> 1) & 3)) * 8;
+        oA[pp] = (min(m0 + r, (int)M - 1) - m0) * (int)lda + sw;
+        oB[pp] = (min(n0 + r, (int)N - 1) - n0) * (int)ldb + sw;
+      }
+    };
+    // the pieces of the stream's next k-step into `slot`; past the end a re-load of the last one.
+    // Issued from inline asm: hipcc cannot tell the slot a ds_read reads from the slots the DMA
+    // fills and, seeing the builtin, waits vmcnt(0) before every k-step's first read -- that would
+    // cut the 2-k-step landing time of each piece to one. The counted waits below order them.
+    auto glds_asm = [](const __bf16* src, const __bf16* dst) {
+      const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(const lds_void*)dst);
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" :: "s"(la), "v"(src) : "m0");
+    };
+    auto pissue = [&](int slot) {
+      const __bf16* a = sA + s_ks * 32;
+      const __bf16* b = sB + s_ks * 32;
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) glds_asm(a + oA[pp], smem + slot * KSL + (wid * 2 + pp) * 512);
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) glds_asm(b + oB[pp], smem + slot * KSL + KSA + (wid * 2 + pp) * 512);
+      if (++s_ks == nks) {
+        if (s_it + 1 < my_tiles) { s_ks = 0; pset(++s_it); }
+        else s_ks = nks - 1;
+      }
+    };
+    bf16x8 fa[MI], fb[NI];
+    auto pread = [&](int slot) {
+      const __bf16* ai = smem + slot * KSL;
+      const __bf16* bi = ai + KSA;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int r = wr * WROWS + i * 16 + li;
+        fa[i] = *reinterpret_cast<const bf16x8*>(ai + r * 32 + ((g ^ ((r >> 1) & 3)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int r = wc * WCOLS + j * 16 + li;
+        fb[j] = *reinterpret_cast<const bf16x8*>(bi + r * 32 + ((g ^ ((r >> 1) & 3)) << 3));
+      }
+    };
+    pset(0);
+    pissue(0);
+    pissue(1);
+    pissue(2);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's pieces of k-step 0
+    asm volatile("s_barrier" ::: "memory");
+    if (grp) asm volatile("s_barrier" ::: "memory");  // waves 4-7: one barrier behind from here on
+    // tiles outer, k-steps inner: the inner loop holds no load hipcc tracks, so the waits it owes to
+    // the epilogue's loads land once before it (a single loop over all k-steps put them, as
+    // vmcnt(0), at the top of every k-step: the DMA of the next two k-steps drained each time)
+    int p = 0;
+    for (int it = 0; it < my_tiles; ++it) {
+      for (int kk = 0; kk < nks; ++kk, ++p) {
+        pread(p & 3);
+        pissue((p + 3) & 3);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // k-step p + 1 landed (this wave's pieces)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(grp && p + 1 == P)) asm volatile("s_barrier" ::: "memory");  // waves 4-7 skip their last
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pend = 0;
+      tile_epilogue(it, 0, 0);
+      pend = 0;
+      // drain the epilogue's stores with a builtin (not asm) wait: hipcc's wait insertion sees it.
+      // Left in flight, the stores' data registers stay pending in hipcc's model and it waits
+      // vmcnt(0) before the first fragment read of every k-step (those registers are reused),
+      // draining the DMA of the next two k-steps each time; here it drains once per tile.
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), expcnt / lgkmcnt unchanged
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stream's trailing re-loads land before exit
+  } else {
   // ---- prologue: k-tiles 0 and 1 in flight, k-tile 0 landed, its first-k-step fragments read
   set_tile_a(0);
   set_tile_b(0);
@@ -1278,6 +1857,10 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   for (int q = 0; q < T; ++q) {
     const int qa1 = qa + 1 == NA ? 0 : qa + 1;
     if (q % nk == 0) COMET_STAMP(q / nk, 0);
+#ifdef COMET_GEMM_STAMPS
+    const bool kst = nk > 4 && q % nk == 3;
+    if (kst) COMET_KSTAMP(q / nk, 3);
+#endif
     // ---- k-step 0 of k-tile q: MFMAs on (a0, b0), reads of the k-step-1 fragments (a1, b1)
     read_frags(qa, q & 1, 1, a1, b1);
     mfmas(a0, b0);
@@ -1291,7 +1874,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     // every wave's reads of buffer q&1 and LDS-DMA of k-tile q+1 are done past this barrier; after
     // an interior tile's epilogue its stores (all issued after that LDS-DMA) stay in flight
 #ifdef COMET_GEMM_STAMPS
-    if (nk > 1 && q % nk == 1) COMET_STAMP(q / nk, 7);  // k-tile 1: before its wait + barrier
+    if (kst) COMET_KSTAMP(q / nk, 4);
 #endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (pend == 2) {  // bf16-park epilogue: 2 x MI stores
@@ -1319,11 +1902,13 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       asm volatile("s_waitcnt vmcnt(%0)" :: "n"(XA) : "memory");
     }
     __builtin_amdgcn_sched_barrier(0);
+#ifdef COMET_GEMM_STAMPS
+    if (kst) COMET_KSTAMP(q / nk, 5);
+#endif
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 #ifdef COMET_GEMM_STAMPS
-    if (q % nk == (nk > 1 ? 1 : 0)) COMET_STAMP(q / nk, 3);
-    if (nk > 1 && q % nk == 0) COMET_STAMP(q / nk, 6);  // k-tile 0 past its barrier
+    if (kst) COMET_KSTAMP(q / nk, 6);
 #endif
     // ---- k-step 1: MFMAs on (a1, b1); LDS-DMA of k-tile q+2 into buffer q&1 (past the end of the
     // stream: a re-load of the last k-tile that nothing reads); reads of k-tile q+1's k-step-0
@@ -1345,459 +1930,17 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       __builtin_amdgcn_sched_group_barrier(SG_MFMA, NMF % NRD, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
+#ifdef COMET_GEMM_STAMPS
+    if (kst) COMET_KSTAMP(q / nk, 7);
+#endif
     advance();
     qa = qa1;
     if (!tile_end) continue;
-    COMET_STAMP(q / nk, 1);
-    // ---- epilogue of tile q / nk, straight from the accumulators: lane (li, g) of fragment
-    // (i, j) holds C[row0 + i*16 + li][col0 + j*16 + 4g + r], r = 0..3
-    int tm, tn;
-    tile_rc(off + (q / nk) * G, tiles_m, tiles_n, tm, tn);
-    const int64_t row0 = (int64_t)tm * TBM + wr * WROWS + li;
-    const int64_t col0 = (int64_t)tn * TBN + wc * WCOLS + 4 * g;
-    const TC* R = reinterpret_cast<const TC*>(epi.resid);
-    TC* X = reinterpret_cast<TC*>(epi.aux);
-    const bool interior = (int64_t)tm * TBM + TBM <= M && (int64_t)tn * TBN + TBN <= N;
-    // loads first (bias, the first residual row), then a store stream with no wait in it: the
-    // residual rows are prefetched one ahead, so their waits only cover the previous row's stores.
-    // Interior tiles take a branch-free copy (no per-store exec branches, whose joins make the
-    // compiler drain every outstanding store before each block).
-    auto epilogue = [&](auto edge_t) {
-      constexpr bool EDGE = decltype(edge_t)::value;
-      const bool bias_c = epi.bias != nullptr;  // per-column bias only (pp_ok)
-      float bc[NI][4];
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bc[j][r] = 0.f;
-      if (bias_c) {  // one uniform branch around straight-line loads (clamped: tail columns never stored)
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int64_t col = col0 + j * 16 + r;
-            bc[j][r] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
-          }
-      }
-      float rc[NI][4], rn[NI][4];
-      auto load_resid = [&](int i, float (&rv)[NI][4]) {
-        const int64_t row = row0 + i * 16;
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int64_t col = col0 + j * 16;
-          if (!EDGE || (row < M && col < N)) load4(R + row * epi.ldr + col, rv[j]);
-        }
-      };
-      if constexpr (HASR) load_resid(0, rc);
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        if constexpr (HASR) {
-          if (i + 1 < MI) load_resid(i + 1, rn);
-        }
-        const int64_t row = row0 + i * 16;
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int64_t col = col0 + j * 16;
-          if (!EDGE || (row < M && col < N)) {
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = epi.alpha * acc[i][j][r] + bc[j][r];
-            if (X) store4(X + row * epi.ldaux + col, v);
-            apply_act_n<4>(ACT, v);
-            if constexpr (HASR) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] += epi.beta * rc[j][r];
-            }
-            store4(C + row * ldc + col, v);
-          }
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        if constexpr (HASR) {
-#pragma unroll
-          for (int j = 0; j < NI; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) rc[j][r] = rn[j][r];
-        }
-      }
-    };
-    if constexpr (LN) {
-      // row-LN epilogue (tiles_n == 1, N == TBN). Pass 1 is the parked pass of the plain f32
-      // epilogue; each lane's final values (8 lanes x NV columns of one row per wave) go back into
-      // the accumulator registers they were parked from, and the lane's row sum and sum of squares
-      // are reduced over the 8 lanes of the row, then over the WN waves of the tile row through
-      // the LDS table st (one barrier; var = E[v^2] - mean^2, clamped at 0). Pass 2 writes the
-      // outputs with the statistics read back per row (no per-row arrays in registers).
-      constexpr int CPL = 4, NTC = WCOLS / (8 * CPL), NV = NTC * CPL;
-      float* park = reinterpret_cast<float*>(smem + RING) + wid * 8 * PPITCH;
-      float* st = reinterpret_cast<float*>(smem + RING + 2 * PARK_F);
-      const int rr = lane >> 3, cc = lane & 7;
-      const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;  // + i*16 + h*8
-      // (tn is always 0 here; keeping it in the column makes the bias / affine loads tile-dependent
-      // so they are not hoisted out of the k-loop, where they would hold ~36 registers)
-      const int pc0 = tn * TBN + wc * WCOLS + cc * CPL;  // + t*8*CPL + e
-      const float invn = 1.f / (float)N;
-      auto VK = [&](int i, int h, int u) -> float { return acc[i][h * NTC + (u >> 2)][u & 3]; };
-      auto lrow = [&](int i, int h) { return (wr * WROWS + i * 16 + h * 8 + rr) * WN; };
-      auto red8 = [](float x) {
-        x += __shfl_xor(x, 1, 64);
-        x += __shfl_xor(x, 2, 64);
-        x += __shfl_xor(x, 4, 64);
-        return x;
-      };
-      // (mean, biased variance) of row (i, h) from the WN (sum, sum of squares) partials
-      auto rowstats = [&](int i, int h, float& mu, float& var) {
-        float x = 0.f, q = 0.f;
-#pragma unroll
-        for (int w = 0; w < WN; ++w) {
-          const float2 p = *reinterpret_cast<const float2*>(st + 2 * (lrow(i, h) + w));
-          x += p.x;
-          q += p.y;
-        }
-        mu = x * invn;
-        var = fmaxf(q * invn - mu * mu, 0.f);
-      };
-      auto lnepilogue = [&](auto edge_t) {
-        constexpr bool EDGE = decltype(edge_t)::value;
-        float bcp[NV];
-#pragma unroll
-        for (int u = 0; u < NV; ++u) bcp[u] = 0.f;
-        if (epi.bias != nullptr) {
-#pragma unroll
-          for (int t = 0; t < NTC; ++t) load4(epi.bias + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(bcp + t * CPL));
-        }
-        // residual rows are loaded one (i, h) step ahead (a 2-slot register ring), so each step's HBM
-        // latency overlaps the previous step's park / reduce / store work instead of being exposed
-        // MI x 2 times (a 3-slot ring measured 4 % slower on the 64 x 384 tiles; round 4: every residual
-        // row of a 64 x 384 tile issued at once, and a 4-slot ring on the 128-row tiles, 1-6 % slower,
-        // profiles/r04_rowln)
-        constexpr int RDL = 2;
-        auto rload = [&](int ih, float (&dst)[NTC][CPL]) {
-          const int64_t row = prow0 + (ih >> 1) * 16 + (ih & 1) * 8;
-#pragma unroll
-          for (int t = 0; t < NTC; ++t)
-#pragma unroll
-            for (int e = 0; e < CPL; ++e) dst[t][e] = 0.f;
-          if constexpr (HASR) {
-#pragma unroll
-            for (int t = 0; t < NTC; ++t)
-              if (!EDGE || row < M) loadn<CPL>(R + row * epi.ldr + pc0 + t * 8 * CPL, dst[t]);
-          }
-        };
-        float rring[RDL][NTC][CPL];
-#pragma unroll
-        for (int d = 0; d < RDL - 1; ++d) rload(d, rring[d]);
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          float vh[2][NV];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int64_t row = prow0 + i * 16 + h * 8;
-            const bool live = !EDGE || row < M;
-            const int ih = 2 * i + h;
-            float (&rc)[NTC][CPL] = rring[ih % RDL];
-            if (ih + RDL - 1 < 2 * MI) rload(ih + RDL - 1, rring[(ih + RDL - 1) % RDL]);
-            if ((li >> 3) == h) {
-#pragma unroll
-              for (int j = 0; j < NI; ++j)
-                *reinterpret_cast<f32x4*>(park + (li & 7) * PPITCH + (((j * 4 + g) ^ pswz(li & 7)) << 2)) = acc[i][j];
-            }
-            asm volatile("" ::: "memory");
-            float s = 0.f, sq = 0.f;
-#pragma unroll
-            for (int t = 0; t < NTC; ++t) {
-              float v[CPL];
-              const int lc = (t * 8 * CPL + cc * CPL) >> 2;
-              const f32x4 p4 = *reinterpret_cast<const f32x4*>(park + rr * PPITCH + ((lc ^ pswz(rr)) << 2));
-              v[0] = p4[0]; v[1] = p4[1]; v[2] = p4[2]; v[3] = p4[3];
-#pragma unroll
-              for (int e = 0; e < CPL; ++e) {
-                float o = apply_act(ACT, epi.alpha * v[e] + bcp[t * CPL + e]);
-                if constexpr (HASR) o += epi.beta * rc[t][e];
-                v[e] = o;
-                vh[h][t * CPL + e] = o;
-                s += o;
-                sq = fmaf(o, o, sq);
-              }
-              if (ln.raw_c && live) storen<CPL>(C + row * ldc + pc0 + t * 8 * CPL, v);
-            }
-            s = red8(s);
-            sq = red8(sq);
-            if (cc == 0) *reinterpret_cast<float2*>(st + 2 * (lrow(i, h) + wc)) = float2{s, sq};
-            asm volatile("" ::: "memory");
-          }
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int t = 0; t < NTC; ++t)
-              acc[i][h * NTC + t] = f32x4{vh[h][4 * t], vh[h][4 * t + 1], vh[h][4 * t + 2], vh[h][4 * t + 3]};
-        }
-        float zw[NV], zb[NV];
-        if (ln.z16 != nullptr) {
-#pragma unroll
-          for (int t = 0; t < NTC; ++t) {
-            load4(ln.zw + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(zw + t * CPL));
-            load4(ln.zb + pc0 + t * 8 * CPL, *reinterpret_cast<float(*)[4]>(zb + t * CPL));
-          }
-        }
-        COMET_STAMP(q / nk, 4);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        COMET_STAMP(q / nk, 5);
-        // pass 2: outputs, row by row (mean / rstd once per row, affine weights loaded before the
-        // barrier: a load issued after this epilogue's stores would wait for them)
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int64_t row = prow0 + i * 16 + h * 8;
-            if (EDGE && row >= M) continue;
-            float mu, var;
-            rowstats(i, h, mu, var);
-            const float ry = rsqrtf(var + ln.eps_y), rz = rsqrtf(var + ln.eps_z);
-#pragma unroll
-            for (int t = 0; t < NTC; ++t) {
-              const int col = pc0 + t * 8 * CPL;
-              float y[CPL];
-#pragma unroll
-              for (int e = 0; e < CPL; ++e) y[e] = (VK(i, h, t * CPL + e) - mu) * ry;
-              if (!ln.raw_c) storen<CPL>(C + row * ldc + col, y);
-              if (ln.y16 != nullptr) store4(ln.y16 + row * ln.ldy + col, y);
-              if (ln.z16 != nullptr) {
-                float z[CPL];
-#pragma unroll
-                for (int e = 0; e < CPL; ++e)
-                  z[e] = (VK(i, h, t * CPL + e) - mu) * rz * zw[t * CPL + e] + zb[t * CPL + e];
-                store4(ln.z16 + row * ln.ldz + col, z);
-              }
-            }
-          }
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      };
-      if (interior) lnepilogue(std::false_type{});
-      else lnepilogue(std::true_type{});
-      // the next tile's k-step-0 fragments again (buffer (q+1)&1 still holds k-tile q+1): the
-      // copies read during k-step 1 are dead here, so their registers serve the epilogue
-      read_frags(qa1, (q + 1) & 1, 0, a0, b0);
-    } else if (BPARK && interior && epi.bpark) {
-      if constexpr (BPARK) {
-        __bf16* slab0 = smem + RING + wid * 2 * BSLAB;
-        const int rr = lane >> 3, cc = lane & 7;
-        float bc[NI][4];
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bc[j][e] = 0.f;
-        if (epi.bias != nullptr) {  // one uniform branch around straight-line loads
-#pragma unroll
-          for (int j = 0; j < NI; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) bc[j][e] = epi.bias[col0 + j * 16 + e];
-        }
-        // per-lane output bases: rows srow0 + i*16 + h*8 (the block offsets are uniform)
-        const int64_t srow0 = (int64_t)tm * TBM + wr * WROWS + rr;
-        const int64_t scol = (int64_t)tn * TBN + wc * WCOLS + cc * 8;
-        TC* cbase = C + srow0 * ldc + scol;
-        // slab layout: row r (0..15) of the block, 16-B chunk k stored at chunk k ^ (r & 7), and the
-        // two 8-B halves of a chunk swapped for rows 8..15 (the fragment writes -- rows li and li + 8
-        // in one lane group -- then hit distinct banks; the row reads are conflict-free)
-        const int wofs = li * WCOLS + ((g & 1) ^ (li >> 3)) * 4;
-        const int rofs = rr * WCOLS + ((cc ^ rr) << 3);
-        // PRE: the activation is applied before parking (no pre-activation copy); otherwise the parked
-        // pre-activation is stored to X and the activation applied to the re-read values. Two
-        // straight-line bodies: a per-element branch on X splits the GELU chains into basic blocks.
-        auto body = [&](auto pre_t) {
-          constexpr bool PRE = decltype(pre_t)::value;
-          TC* xbase = PRE ? nullptr : X + srow0 * epi.ldaux + scol;
-#pragma unroll
-          for (int i = 0; i < MI; ++i) {
-            __bf16* slab = slab0 + (i & 1) * BSLAB;
-#pragma unroll
-            for (int j = 0; j < NI; ++j) {
-              float v[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                v[e] = epi.alpha * acc[i][j][e] + bc[j][e];
-                if constexpr (PRE) v[e] = apply_act(ACT, v[e]);
-              }
-              *reinterpret_cast<uint2*>(slab + wofs + (((2 * j + (g >> 1)) ^ (li & 7)) << 3)) =
-                  uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-              acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              uint4 d = *reinterpret_cast<const uint4*>(slab + h * 8 * WCOLS + rofs);
-              if (h == 1) d = uint4{d.z, d.w, d.x, d.y};
-              const int64_t roff = (int64_t)(i * 16 + h * 8);
-              if constexpr (!PRE) {
-                *reinterpret_cast<uint4*>(xbase + roff * epi.ldaux) = d;
-                const unsigned u[4] = {d.x, d.y, d.z, d.w};
-                unsigned o[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                  o[e] = pack_bf16x2(apply_act(ACT, bf16_lo(u[e])), apply_act(ACT, bf16_hi(u[e])));
-                d = uint4{o[0], o[1], o[2], o[3]};
-              }
-              *reinterpret_cast<uint4*>(cbase + roff * ldc) = d;
-            }
-            asm volatile("" ::: "memory");
-          }
-        };
-        if (X == nullptr) body(std::true_type{});
-        else body(std::false_type{});
-        read_frags(qa1, (q + 1) & 1, 0, a0, b0);
-      }
-    } else if constexpr (BPARK) {
-      epilogue(std::true_type{});  // edge tiles (or unaligned outputs): masked direct stores
-    } else if constexpr (PARK) {
-      // parked epilogue: per 8-row half of each 16-row block the wave parks its 8 x WCOLS raw
-      // accumulators in its own LDS slab (no barrier: only this wave touches it) and re-reads them
-      // row-contiguously, so every store / residual load instruction covers 8 rows x 128 B
-      constexpr int CPL = 16 / (int)sizeof(TC);       // output columns per lane per access (16 B)
-      constexpr int NTC = WCOLS / (8 * CPL);          // column passes per row
-      float* park = reinterpret_cast<float*>(smem + RING) + wid * 8 * PPITCH;
-      const int rr = lane >> 3, cc = lane & 7;
-      const int64_t prow0 = (int64_t)tm * TBM + wr * WROWS + rr;        // + i*16 + h*8
-      const int64_t pcol0 = (int64_t)tn * TBN + wc * WCOLS + cc * CPL;  // + t*8*CPL
-      auto pepilogue = [&](auto edge_t) {
-        constexpr bool EDGE = decltype(edge_t)::value;
-        const bool bias_c = epi.bias != nullptr;  // per-column bias only (pp_ok)
-        float bcp[NTC][CPL];
-#pragma unroll
-        for (int t = 0; t < NTC; ++t)
-#pragma unroll
-          for (int e = 0; e < CPL; ++e) bcp[t][e] = 0.f;
-        if (bias_c) {
-#pragma unroll
-          for (int t = 0; t < NTC; ++t)
-#pragma unroll
-            for (int e = 0; e < CPL; ++e) {
-              const int64_t col = pcol0 + t * 8 * CPL + e;
-              bcp[t][e] = epi.bias[EDGE ? (col < N ? col : N - 1) : col];
-            }
-        }
-        // residual rows prefetched RD (i, h) steps ahead into a register ring (the next tile's
-        // k-step-0 fragments are re-read after the epilogue, so their registers hold the ring):
-        // each step's residual load then has RD - 1 steps of park / store work to land in (3 steps:
-        // epilogue 39.5k -> 32.1k cycles per 256 x 256 f32 tile, K 3072 GEMM 835 -> 900 TF/s)
-        constexpr int NSTEP = 2 * MI, RD = HASR ? 4 : 1;
-        float rq[RD][NTC][CPL];
-        auto rld = [&](int st, float (&dst)[NTC][CPL]) {
-          const int64_t row = prow0 + (st >> 1) * 16 + (st & 1) * 8;
-#pragma unroll
-          for (int t = 0; t < NTC; ++t) {
-            const int64_t col = pcol0 + t * 8 * CPL;
-            if (!EDGE || (row < M && col < N)) loadn<CPL>(R + row * epi.ldr + col, dst[t]);
-          }
-        };
-        if constexpr (HASR) {
-#pragma unroll
-          for (int d = 0; d < RD; ++d)
-            if (d < NSTEP) rld(d, rq[d]);
-        }
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            float (&rc)[NTC][CPL] = rq[(2 * i + h) % RD];
-            const int64_t row = prow0 + i * 16 + h * 8;
-            if ((li >> 3) == h) {
-#pragma unroll
-              for (int j = 0; j < NI; ++j)
-                *reinterpret_cast<f32x4*>(park + (li & 7) * PPITCH + (((j * 4 + g) ^ pswz(li & 7)) << 2)) = acc[i][j];
-            }
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int t = 0; t < NTC; ++t) {
-              const int64_t col = pcol0 + t * 8 * CPL;
-              float v[CPL];
-#pragma unroll
-              for (int e = 0; e < CPL; e += 4) {
-                const int lc = (t * 8 * CPL + cc * CPL + e) >> 2;
-                const f32x4 p4 = *reinterpret_cast<const f32x4*>(park + rr * PPITCH + ((lc ^ pswz(rr)) << 2));
-                v[e] = p4[0]; v[e + 1] = p4[1]; v[e + 2] = p4[2]; v[e + 3] = p4[3];
-              }
-              if (!EDGE || (row < M && col < N)) {
-#pragma unroll
-                for (int e = 0; e < CPL; ++e) v[e] = epi.alpha * v[e] + bcp[t][e];
-                if (X) storen<CPL>(X + row * epi.ldaux + col, v);
-                apply_act_n<CPL>(ACT, v);
-                if constexpr (HASR) {
-#pragma unroll
-                  for (int e = 0; e < CPL; ++e) v[e] += epi.beta * rc[t][e];
-                }
-                storen<CPL>(C + row * ldc + col, v);
-              }
-            }
-            if constexpr (HASR) {
-              if (2 * i + h + RD < NSTEP) rld(2 * i + h + RD, rc);
-            }
-            asm volatile("" ::: "memory");
-            if (h == 1) {
-#pragma unroll
-              for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-          }
-      };
-      if (interior) pepilogue(std::false_type{});
-      else pepilogue(std::true_type{});
-      if constexpr (HASR) read_frags(qa1, (q + 1) & 1, 0, a0, b0);
-    } else {
-    if constexpr (WIDE) {
-      if (interior && X == nullptr && epi.wide) {
-        // lane (li, g) of fragment (i, j) holds row li, columns 16j + 4g .. +3 (bf16-packed as uint2);
-        // permlane16_swap(frag j, frag j+1) exchanges 16-lane groups 1 <-> 0 and 3 <-> 2, after which
-        // group g holds 8 contiguous columns: 16(j + (g & 1)) + 8(g >> 1) .. +7
-        const bool bias_c = epi.bias != nullptr;
-        float bc[NI][4];
-#pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bc[j][e] = bias_c ? epi.bias[col0 + j * 16 + e] : 0.f;
-        const int64_t wcol = (int64_t)tn * TBN + wc * WCOLS + 16 * (g & 1) + 8 * (g >> 1);
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int64_t row = row0 + i * 16;
-#pragma unroll
-          for (int j = 0; j < NI; j += 2) {
-            unsigned pk[2][2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              float v[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = epi.alpha * acc[i][j + u][e] + bc[j + u][e];
-              apply_act_n<4>(ACT, v);
-              pk[u][0] = pack_bf16x2(v[0], v[1]);
-              pk[u][1] = pack_bf16x2(v[2], v[3]);
-              acc[i][j + u] = f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-            const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
-            const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-            *reinterpret_cast<uint4*>(C + row * ldc + wcol + 16 * j) = uint4{s0[0], s1[0], s0[1], s1[1]};
-          }
-        }
-      } else if (interior) {
-        epilogue(std::false_type{});
-      } else {
-        epilogue(std::true_type{});
-      }
-    } else {
-    if (interior) epilogue(std::false_type{});
-    else epilogue(std::true_type{});
-    }
-    }
-    // interior: every VMEM op this epilogue issued came after the LDS-DMA of k-tile q+2 and their
-    // count is fixed, so the next barrier wait leaves them in flight
-    if (BPARK && interior && epi.bpark) pend = X != nullptr ? 3 : 2;
-    else if constexpr (WIDE) pend = (interior && X == nullptr && epi.wide) ? 1 : 0;
-    else pend = interior ? 1 : 0;
-    COMET_STAMP(q / nk, 2);
+    tile_epilogue(q / nk, q, qa1);
+  }
   }
 #ifdef COMET_GEMM_STAMPS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  COMET_STAMP(my_tiles, 3);
 #endif
 }
 }  // namespace w4
@@ -2024,14 +2167,23 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   COMET_CHECK_ARG(tiles_m * tiles_n < (1ll << 30), "comet_gemm: too many tiles");
   const int ntiles = (int)(tiles_m * tiles_n);
   if (ntiles <= grid) grid = ntiles;
-#define PPKT(ACT, HR, BMT, BNT)                                                                               \
-  hipLaunchKernelGGL((w4::gemm_w4_kernel<TC, ACT, HR, 8, BMT, BNT>), dim3((unsigned)grid), dim3(512), 0, s,   \
+  // 256 x 256 tiles: the ping-pong k-loop (PING instances) for long-K bf16 outputs without a
+  // residual (profiles/r05_n: 8192^3 +8..14 %, K 768 0..+4 %, K <= 384 5-9 % slower -- the tile's two
+  // wave groups then run their epilogues one after the other and drain the stores once per tile;
+  // the f32 + residual K 3072 shape even). COMET_GEMM_PING=1 / =0 forces it on / off (measurement).
+  static const char* ping_env = getenv("COMET_GEMM_PING");
+  const bool ping = ping_env != nullptr ? ping_env[0] == '1'
+                                        : (a.k >= 2048 && a.dtype_c == COMET_BF16 && a.resid == nullptr);
+#define PPKT(ACT, HR, BMT, BNT, PG)                                                                           \
+  hipLaunchKernelGGL((w4::gemm_w4_kernel<TC, ACT, HR, 8, BMT, BNT, false, PG>), dim3((unsigned)grid), dim3(512), 0, s, \
                      (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, a.n, a.k,     \
                      (int)tiles_n, ntiles, e, noln)
 #define PPK(ACT, HR)                                                                                          \
   do {                                                                                                        \
-    if (n384) { if (half) PPKT(ACT, HR, 64, 384); else PPKT(ACT, HR, 128, 384); }                           \
-    else { if (half) PPKT(ACT, HR, 128, 256); else PPKT(ACT, HR, 256, 256); }                               \
+    if (n384) { if (half) PPKT(ACT, HR, 64, 384, false); else PPKT(ACT, HR, 128, 384, false); }             \
+    else if (half) PPKT(ACT, HR, 128, 256, false);                                                            \
+    else if (ping) PPKT(ACT, HR, 256, 256, true);                                                             \
+    else PPKT(ACT, HR, 256, 256, false);                                                                      \
   } while (0)
 #define PPR(ACT) do { if (a.resid) PPK(ACT, true); else PPK(ACT, false); } while (0)
   switch (a.act) {

@@ -192,6 +192,7 @@ def _rank(rank, world, port, q, paths, size):
         res = []
         for step in range(2):  # step 0 = bucket discovery, step 1 = rebuilt buckets with overlap
             model.zero_grad(set_to_none=True)
+            bk.record = step == 1
             bk.prepare_backward()
             fwd_bwd()
             bk.finish_backward()
@@ -202,14 +203,17 @@ def _rank(rank, world, port, q, paths, size):
             # descriptor that vanishes when this process exits before the parent reads it
             g = {k: p.grad.detach().cpu().numpy().copy() for k, p in model.camera_predictor.named_parameters()
                  if p.grad is not None and k in SELECT}
+        # this step's own local gradients, as the buckets held them before the exchange
+        pre = {k: bk.pre_reduce_grad(p).detach().cpu().numpy().copy()
+               for k, p in model.camera_predictor.named_parameters() if p.grad is not None and k in SELECT}
         during = all(d for _, d in bk.launch_log)
         print(f"{size} rank {rank}: B={br}, {len(bk.buckets)} buckets, peak device memory "
               f"{torch.cuda.max_memory_allocated() / 2**30:.1f} GiB", flush=True)
-        q.put((rank, res, g, during, len(bk.buckets), local, again))
+        q.put((rank, res, g, during, len(bk.buckets), local, again, pre))
         dist.destroy_process_group()
     except Exception as e:  # surface the error to the parent
         import traceback
-        q.put((rank, None, traceback.format_exc(), None, None, None, None))
+        q.put((rank, None, traceback.format_exc(), None, None, None, None, None))
         raise
 
 
@@ -228,23 +232,32 @@ def test_ddp_simulated_ranks_equal_B2_gradients(size):
         p.start()
     got = {}
     for _ in range(2):
-        rank, res, g, during, nb, local, again = q.get(timeout=600)
+        rank, res, g, during, nb, local, again, pre = q.get(timeout=600)
         assert res is not None, g
-        got[rank] = (res, g, during, nb, local)
+        got[rank] = (res, g, during, nb, local, pre)
         for k, v in again.items():
             print(f"{size} rank {rank} {k}: second local pass vs first rel-to-max {v:.2e}")
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # (a) the exchange: reduced == mean of the local gradients
-    errs = []
+    # (a) the exchange: reduced == mean of the ranks' local gradients of the same step (the buckets
+    # just before their all-reduce): exact up to the summation order
+    errs, runs = [], []
     for rank in (0, 1):
         for k, v in got[rank][1].items():
-            mean = (got[0][4][k].astype(np.float64) + got[1][4][k].astype(np.float64)) / 2
+            mean = (got[0][5][k].astype(np.float64) + got[1][5][k].astype(np.float64)) / 2
             err = np.abs(v - mean).max() / max(np.abs(mean).max(), 1e-30)
-            print(f"{size} rank {rank} {k}: reduced vs mean(local) rel-to-max {err:.2e}")
+            print(f"{size} rank {rank} {k}: reduced vs mean(pre-reduce local) rel-to-max {err:.2e}")
             errs.append((err, rank, k))
+            # the separate local pass before the bucketer: the same gradients up to the run-to-run
+            # variation two ranks sharing one GPU show (bf16: ~1e-3; one process alone repeats to
+            # the f32 atomics' 1e-7, tools/determinism.py, profiles/r05_h)
+            loc = got[rank][4][k].astype(np.float64)
+            run = np.abs(got[rank][5][k] - loc).max() / max(np.abs(loc).max(), 1e-30)
+            print(f"{size} rank {rank} {k}: pre-reduce vs separate local pass rel-to-max {run:.2e}")
+            runs.append((run, rank, k))
     assert max(errs)[0] < 1e-5, max(errs)
+    assert max(runs)[0] < (2e-2 if SIZES[size][4] == torch.bfloat16 else 1e-4), max(runs)
     # (b) single process, B = 2
     seed, T, S, N, dtype, _ = SIZES[size]
     model, cfg = _model()
@@ -260,7 +273,7 @@ def test_ddp_simulated_ranks_equal_B2_gradients(size):
     floor = 1e-6
     worst = 0.0
     for rank in (0, 1):
-        res, g, during, nb, _ = got[rank]
+        res, g, during, nb, _, _ = got[rank]
         assert during and nb > 1, "rebuilt buckets must all launch during the backward"
         for step in (0, 1):
             assert set(res[step]) == set(ref)

@@ -7,5 +7,5 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 600 python -u tools/race_stress.py ${REPS:-40} > $O/race.txt 2>&1
+timeout -k 10 600 python -u tools/race_stress.py ${REPS:-200} > $O/race.txt 2>&1
 rc=$?; grep -v amdgpu.ids $O/race.txt; echo "race rc $rc"

@@ -18,13 +18,24 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "comet-pose-estimation_amd")]
 
 
 def noise(seconds):
+    # HBM streaming plus co-resident compute (vendor GEMMs using LDS and every CU): the other
+    # process's workgroups then share the CUs with the ops under test and perturb their waves'
+    # relative timing, as a second rank on the same device does
     a = torch.empty(512 * 2**20, device="cuda", dtype=torch.float32)  # 2 GiB
     b = torch.empty_like(a)
+    x = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
+    y = torch.randn(4096, 4096, device="cuda", dtype=torch.bfloat16)
     t0 = time.time()
+    first = True
     while time.time() - t0 < seconds:
-        for _ in range(20):
+        if first:
+            print("noise running", flush=True)
+            first = False
+        for _ in range(10):
             b.copy_(a)
+            z = x @ y
             a.copy_(b)
+            z = z @ y
         torch.cuda.synchronize()
 
 
@@ -95,9 +106,10 @@ def main():
         return
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     flt = sys.argv[2] if len(sys.argv) > 2 else ""
-    nz = subprocess.Popen([sys.executable, __file__, "--noise", "600"])
+    nz = subprocess.Popen([sys.executable, __file__, "--noise", "600"], stdout=subprocess.PIPE, text=True)
     try:
-        time.sleep(3)
+        assert nz.stdout.readline().strip() == "noise running", "noise process did not start"
+        print("noise process running", flush=True)
         bad = 0
         for name, f in cases():
             if flt not in name:
