@@ -72,11 +72,11 @@ def instance(name):
         if base == "gemm_big_kernel":
             tc, bn, la, lb, split = a[0], a[1], a[2], a[3], a[4]
             return f"comet_gemm|big{bn}.L{la}{lb}.{'split' if split == 'true' else tc}"
-        if base == "gemm_w4_kernel":  # <TC, ACT, HASR, NW, TBM, TBN, LN>
+        if base == "gemm_w4_kernel":  # <TC, ACT, HASR, NW, TBM, TBN, LN, PING>
             # index from the end: the demangler sometimes splits an enum ACT argument in two
-            if a[-1] == "true":
+            if a[-2] == "true":
                 return "comet_gemm_rowln"
-            return f"comet_gemm|pp{a[-3]}x{a[-2]}.L00.{a[0]}"
+            return f"comet_gemm|pp{a[-4]}x{a[-3]}.L00.{a[0]}"
         if base == "gemm_bf16_kernel":
             tc, la, lb, split, conv = a[0], a[1], a[2], a[5], a[6]
             if conv == "true":

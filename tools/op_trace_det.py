@@ -1,0 +1,94 @@
+"""Find the first kernel whose output differs between repeated forward passes: every public
+function of comet_amd.ops is wrapped to record a byte checksum of each tensor it returns (and of its
+`out=` tensor); the model forward runs three times on identical inputs and weights, and the first
+call index whose checksums differ from pass 0 is printed with its op name and argument shapes.
+Run two of these at once to reproduce the two-ranks-on-one-device variation (profiles/r05_h).
+
+    python tools/op_trace_det.py [bf16|fp32]
+"""
+import functools
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "comet-pose-estimation_amd")]
+
+REC = []
+
+
+def _sum(t):
+    if not torch.is_tensor(t) or not t.is_cuda or t.numel() == 0:
+        return None
+    b = t.detach().contiguous().view(-1)
+    if b.dtype in (torch.float32, torch.int32):
+        b = b.view(torch.int32)
+    elif b.dtype in (torch.bfloat16, torch.float16, torch.int16):
+        b = b.view(torch.int16)
+    else:
+        b = b.to(torch.int64)
+    # position-weighted integer checksum (order-sensitive), on the device, no sync
+    w = torch.arange(1, b.numel() + 1, device=b.device, dtype=torch.int64) % 1000003
+    return (b.to(torch.int64) * w).sum()
+
+
+def _shape(a):
+    return tuple(a.shape) if torch.is_tensor(a) else type(a).__name__
+
+
+def wrap(name, fn):
+    @functools.wraps(fn)
+    def w(*args, **kw):
+        r = fn(*args, **kw)
+        outs = list(r) if isinstance(r, (tuple, list)) else [r]
+        if "out" in kw:
+            outs.append(kw["out"])
+        sums = [s for s in (_sum(o) for o in outs) if s is not None]
+        REC.append((name, [_shape(a) for a in args[:4]], sums))
+        return r
+    return w
+
+
+def main():
+    from comet_amd import functional as F, ops
+    from comet_amd.config import instantiate, load_config
+    from comet_amd.models.utils import QuaternionCameras
+    from oracle import prng
+    from oracle.weights import comet_shapes
+    for k in dir(ops):
+        v = getattr(ops, k)
+        if callable(v) and not k.startswith("_") and getattr(v, "__module__", "") == ops.__name__ and k not in ("stream", "dt"):
+            setattr(ops, k, wrap(k, v))
+    dtype = torch.float32 if len(sys.argv) > 1 and sys.argv[1] == "fp32" else torch.bfloat16
+    T, S, N = 16, 512, 512
+    cfg = load_config()
+    torch.manual_seed(0)
+    model = instantiate(cfg.MODEL, _recursive_=False, cfg=cfg)
+    model.load_state_dict(prng.make_state_dict(0, comet_shapes()), strict=True)
+    model = model.cuda()
+    img, tracks, gt = prng.synthetic_batch(37, 1, T, S, S, N)
+    img, tracks = img.cuda(), tracks.cuda()
+    cams = QuaternionCameras(R=gt["R"], T_uvz=gt["T_uvz"], T=gt["T"], focal_length=gt["focal_length"],
+                             principal_point=gt["principal_point"], ratio=gt["ratio"], device="cuda")
+    passes = []
+    for it in range(3):
+        REC.clear()
+        with F.precision(dtype), torch.no_grad():
+            model(img, gt_cameras=cams, training=True, tracks=tracks)
+        torch.cuda.synchronize()
+        passes.append([(n, shp, [int(s.item()) for s in sums]) for n, shp, sums in REC])
+    for it in (1, 2):
+        a, b = passes[0], passes[it]
+        first = next((i for i, (x, y) in enumerate(zip(a, b)) if x[2] != y[2]), None)
+        if first is None and len(a) == len(b):
+            print(f"pass {it}: all {len(a)} op outputs identical to pass 0", flush=True)
+        else:
+            print(f"pass {it}: first differing op output at call {first} of {len(a)}: {a[first][0]} {a[first][1]}", flush=True)
+            diffs = [i for i, (x, y) in enumerate(zip(a, b)) if x[2] != y[2]]
+            print(f"   {len(diffs)} differing calls; first ten: " +
+                  ", ".join(f"{i}:{a[i][0]}" for i in diffs[:10]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
