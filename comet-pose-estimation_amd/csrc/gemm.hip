@@ -2133,6 +2133,8 @@ int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s
   // tracker's virtual tracks): every CU gets a tile. Default since round 5 (2-5 % faster on every
   // M = 8192 shape, same box, profiles/r05_rowln); COMET_ROWLN_NO32=1 keeps the 64-row tiles
   if (tbn == 384 && tbm == 64 && 2 * cdiv(a.m, 64) <= grid && getenv("COMET_ROWLN_NO32") == nullptr) tbm = 32;
+  // measurement: 32-row tiles for every N = 384 shape (COMET_ROWLN_32ALL=1)
+  if (tbn == 384 && tbm == 64 && getenv("COMET_ROWLN_32ALL") != nullptr) tbm = 32;
   const int64_t tiles_m = cdiv(a.m, tbm);
   COMET_CHECK_ARG(tbn == a.n && tiles_m < (1ll << 30), "comet_gemm_rowln: the row must fit one tile");
   const int ntiles = (int)tiles_m;
