@@ -259,3 +259,65 @@ def test_backward_outside_prepare_stays_local():
         for k, p in net.named_parameters():
             if p.grad is not None:
                 torch.testing.assert_close(torch.from_numpy(got[rank][k]), p.grad, rtol=1e-6, atol=1e-7)
+
+
+def _record_worker(rank, world, port, q, paths):
+    import sys
+    sys.path[:0] = paths
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from comet_amd.ddp import GradBucketer
+        net = _Net()
+        bk = GradBucketer(net.parameters(), bucket_mb=0.004)
+        res = []
+        for step in range(2):  # discovery, then the rebuilt buckets
+            bk.record = True
+            bk.prepare_backward()
+            x, y = _data(rank, step)
+            ((net(x) - y) ** 2).mean().backward()
+            bk.finish_backward()
+            if step == 1:
+                pre = {k: bk.pre_reduce_grad(p).detach().numpy().copy() for k, p in net.named_parameters()
+                       if p.grad is not None}
+                red = {k: p.grad.detach().numpy().copy() for k, p in net.named_parameters() if p.grad is not None}
+                res = (pre, red)
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_record_keeps_pre_reduce_gradients():
+    """GradBucketer.record: each bucket's copy taken just before its all-reduce holds this rank's own
+    (local) gradient, and the reduced gradient is the mean of those copies over the ranks -- the
+    exact exchange check the GPU simulated-ranks test uses (tests/test_configs_gpu.py)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_record_worker, args=(r, world, port, q, [ROOT, PKG])) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, res = q.get(timeout=120)
+        got[rank] = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the local gradient of each rank at step 1
+    net = _Net()
+    local = {}
+    for r in range(world):
+        net.zero_grad(set_to_none=True)
+        x, y = _data(r, 1)
+        ((net(x) - y) ** 2).mean().backward()
+        local[r] = {k: p.grad.clone() for k, p in net.named_parameters() if p.grad is not None}
+    assert set(got[0][0]) == set(local[0])
+    for r in range(world):
+        pre, red = got[r]
+        for k in pre:
+            torch.testing.assert_close(torch.from_numpy(pre[k]), local[r][k], rtol=1e-6, atol=1e-7)
+            mean = (torch.from_numpy(got[0][0][k]) + torch.from_numpy(got[1][0][k])) / 2
+            torch.testing.assert_close(torch.from_numpy(red[k]), mean, rtol=1e-6, atol=1e-7)
