@@ -2170,14 +2170,16 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   const int ntiles = (int)(tiles_m * tiles_n);
   if (ntiles <= grid) grid = ntiles;
   // 256 x 256 tiles: the ping-pong k-loop (PING instances) for bf16 outputs without activation,
-  // residual or pre-activation copy at K >= 768 (profiles/r05_n: 8192^3 +8..14 %, M 74368 N 2304 K 768
-  // +4 %; with GELU at K 768 and the f32 + residual K 3072 shape even, K <= 384 5-9 % slower -- the
-  // tile's two wave groups then run their epilogues one after the other and drain the stores once
-  // per tile). COMET_GEMM_PING=1 / =0 forces it on / off (measurement).
+  // residual or pre-activation copy at K >= 768, and for any output / residual at K >= 2048
+  // (profiles/r05_n: 8192^3 +8..14 %, M 74368 N 2304 K 768 +4 %, the f32 + residual K 3072 shape
+  // +1..2 %; with GELU at K 768 even, K <= 384 5-9 % slower -- the tile's two wave groups then run
+  // their epilogues one after the other and drain the stores once per tile). COMET_GEMM_PING=1 / =0
+  // forces it on / off (measurement).
   static const char* ping_env = getenv("COMET_GEMM_PING");
   const bool ping = ping_env != nullptr ? ping_env[0] == '1'
-                                        : (a.k >= 768 && a.dtype_c == COMET_BF16 && a.resid == nullptr &&
-                                           a.aux == nullptr && a.act == COMET_ACT_NONE);
+                                        : (a.aux == nullptr && a.act == COMET_ACT_NONE &&
+                                           ((a.k >= 768 && a.dtype_c == COMET_BF16 && a.resid == nullptr) ||
+                                            a.k >= 2048));
 #define PPKT(ACT, HR, BMT, BNT, PG)                                                                           \
   hipLaunchKernelGGL((w4::gemm_w4_kernel<TC, ACT, HR, 8, BMT, BNT, false, PG>), dim3((unsigned)grid), dim3(512), 0, s, \
                      (const __bf16*)a.a, a.lda, (const __bf16*)a.b, a.ldb, (TC*)a.c, a.ldc, a.m, a.n, a.k,     \
