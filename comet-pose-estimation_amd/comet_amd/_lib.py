@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("COMET_HIP_LIB", os.path.join(os.path.dirname(_HERE), 
 F32 = 0
 BF16 = 1
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_SIGMOID = 0, 1, 2, 3
+SQ_NORM_PARTIALS = 1024  # COMET_SQ_NORM_PARTIALS: scratch floats of comet_sq_norm_multi
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32
@@ -92,6 +93,8 @@ _INT = ctypes.c_int
 SIGNATURES = {
     "comet_count_nonfinite": (_INT, [_INT, c_vp, c_i64, c_vp, c_vp]),
     "comet_debug_flags": (_INT, [_INT]),
+    "comet_lds_probe": (_INT, [_INT, _INT, _INT, c_vp, c_vp]),
+    "comet_shfl_probe": (_INT, [_INT, _INT, _INT, c_vp, c_vp]),
     "comet_version": (_INT, []),
     "comet_last_error": (ctypes.c_char_p, []),
     "comet_gemm": (_INT, [ctypes.POINTER(GemmArgs), c_vp]),
@@ -120,7 +123,7 @@ SIGNATURES = {
     "comet_axpby": (_INT, [c_vp, c_vp, _F, _F, c_i64, c_vp]),
     "comet_act_bwd_colsum": (_INT, [_INT, _INT, c_vp, _INT, c_vp, _INT, c_vp, c_vp, c_i64, c_i64, _INT, c_vp]),
     "comet_colsum": (_INT, [_INT, c_vp, c_vp, c_i64, c_i64, c_i64, _INT, c_vp]),
-    "comet_sq_norm_multi": (_INT, [c_vp, c_vp, _INT, c_vp, c_vp]),
+    "comet_sq_norm_multi": (_INT, [c_vp, c_vp, _INT, c_vp, c_vp, c_vp]),
     "comet_adamw_multi": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, _INT, _F, _F, _F, _F, _F, _INT, c_vp, _F, c_vp]),
     "comet_im2col_nhwc": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _INT, _INT, _INT, _INT, c_i64, c_i64, c_i64, c_vp]),
     "comet_instnorm_workspace": (_INT, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),

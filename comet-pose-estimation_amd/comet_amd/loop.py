@@ -188,7 +188,7 @@ class _BatchShard(torch.utils.data.Sampler):
       * even_batches=True (accelerate's default): the last round is completed -- and a short last
         batch filled -- with indices cycled from the start of the epoch (the first `world` batches),
         so every rank runs the same number of steps on full batches;
-      * even_batches=False (abl_ours.py:28): the last round's batches go to the first ranks as they
+      * even_batches=False (train_e2epose2.py:47, abl_ours.py:28): the last round's batches go to the first ranks as they
         are, so the last ranks may run one batch fewer.
     `batch_size` / `drop_last` are read from the wrapped sampler (a plain list of batches: batch size
     None -- variable-length batches, cycled whole -- and drop_last False), as accelerate does.
@@ -259,8 +259,9 @@ class _BatchShard(torch.utils.data.Sampler):
 
 class CometAccelerator:
     """accelerate.Accelerator subset of the reference's loops. Batches shard over ranks as
-    accelerate's BatchSamplerShard does (_BatchShard): even_batches=True (train_e2epose2.py) completes
-    the last round with samples cycled from the epoch's start; even_batches=False (abl_ours.py:28)
+    accelerate's BatchSamplerShard does (_BatchShard): even_batches=True (accelerate's default)
+    completes the last round with samples cycled from the epoch's start; even_batches=False (what
+    every reference entry point passes: train_e2epose2.py:47, abl_ours.py:28, test_e2epose2.py:29)
     keeps the batches that do not fill every rank, so the last ranks may run one batch fewer."""
 
     def __init__(self, mixed_precision="no", device=None, bucket_mb=25, even_batches=True):
@@ -503,7 +504,9 @@ def train_fn(cfg, data_root=None, eval_only=True, csv_log=True):
     ckpt_interval epochs, eval every eval_interval epochs, a final checkpoint)."""
     from .config import instantiate
     from .train import build_optimizer
-    acc = CometAccelerator(mixed_precision=_get(cfg, "mixed_precision", "no"))
+    # train_e2epose2.py:47: Accelerator(even_batches=False, ...) -- with the train loader's
+    # drop_last=True the shards are the same either way; a loader without it keeps its tail batches
+    acc = CometAccelerator(mixed_precision=_get(cfg, "mixed_precision", "no"), even_batches=False)
     set_seed_and_print(int(_get(cfg, "seed", 0)))
     exp_dir = _get(cfg, "exp_dir", "exp")
     logger = None

@@ -65,7 +65,7 @@ def _res_ln(x, w, b, resid, raw=True, y16_eps=None, z=None):
     LayerNorm kernels separately, same outputs). y16 / z16 are in the compute dtype."""
     wc = F.wcast(w)
     xc = x if x.dtype == wc.dtype else ops.cast(x, wc.dtype)
-    if ops.linear_rowln_ok(xc, wc, resid):
+    if ops.linear_rowln_ok(xc, wc, resid, bias=b, z=z):
         return ops.linear_rowln(xc, wc, b, resid, raw=raw, y16_eps=y16_eps, z=z)
     cdt = F.compute_dtype()
     c = ops.linear(xc, wc, bias=b, resid=resid, out_dtype=torch.float32)

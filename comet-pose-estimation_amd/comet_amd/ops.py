@@ -181,17 +181,22 @@ def _rowln_args(x2, wc, o2, bias, r2):
     return g
 
 
-def linear_rowln_ok(x, w, resid):
+def linear_rowln_ok(x, w, resid, bias=None, z=None):
     """True when comet_gemm_rowln takes this Linear (bf16 operands, f32 residual output, N in
-    {256, 384}, K % 64 == 0, M >= 4096; see include/comet_hip.h)."""
+    {256, 384}, K % 64 == 0, M >= 4096, 16-B aligned bias / affine LN vectors; see
+    include/comet_hip.h)."""
     if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or resid is None or resid.dtype != torch.float32:
         return False
     K, N = x.shape[-1], w.shape[0]
     if N not in (256, 384) or resid.shape[-1] != N or x.stride(-1) != 1 or w.stride(-1) != 1:
         return False
+    # the kernel reads bias and the affine LN weight / shift four columns (16 B) at a time
+    for t in (bias, *(z[:2] if z is not None else ())):
+        if t is not None and (t.data_ptr() % 16 != 0 or t.dtype != torch.float32 or not t.is_contiguous()):
+            return False
     x2 = x.reshape(-1, K)
     r2 = resid.reshape(-1, N)
-    g = _rowln_args(x2, w, r2, None, r2)
+    g = _rowln_args(x2, w, r2, bias, r2)
     return bool(L.load().comet_gemm_rowln_ok(ctypes.byref(g)))
 
 

@@ -117,11 +117,14 @@ class CometAdamW(torch.optim.Optimizer):
             if g.dtype != torch.float32 or not g.is_contiguous() or g.device != ps[0].device:
                 raise L.CometHipError(f"CometAdamW: gradients must be contiguous float32 on {ps[0].device}; got "
                                       f"{g.dtype} on {g.device} (contiguous={g.is_contiguous()})")
-        out = torch.zeros(1, device=ps[0].device, dtype=torch.float32)
+        # out[0] and the per-workgroup partials of the fixed-order reduction in one allocation
+        buf = torch.zeros(1 + L.SQ_NORM_PARTIALS, device=ps[0].device, dtype=torch.float32)
+        out = buf[:1]
         arr = (ctypes.c_void_p * len(ps))(*[p.grad.data_ptr() for p in ps])
         sz = (ctypes.c_int64 * len(ps))(*[p.numel() for p in ps])
         e0 = PROF.start()
-        L.check(L.load().comet_sq_norm_multi(arr, sz, len(ps), out.data_ptr(), ops.stream()), "sq_norm")
+        L.check(L.load().comet_sq_norm_multi(arr, sz, len(ps), out.data_ptr(), buf[1:].data_ptr(), ops.stream()),
+                "sq_norm")
         PROF.stop(e0, "comet_sq_norm_multi", 0.0, 4.0 * sum(p.numel() for p in ps))
         return out
 

@@ -172,10 +172,14 @@ struct MultiPtr {
   int count;
 };
 
-// Few workgroups (SQ_NORM_BLOCKS) and 16-B loads: the sum ends in one atomic per workgroup on a
-// single address, and 8192 of them serialised at L2 cost ~90 us per launch.
-constexpr int SQ_NORM_BLOCKS = 1024;
-__global__ void sq_norm_kernel(MultiPtr mp, float* __restrict__ out) {
+// Squared L2 norm of many tensors in a fixed summation order (the clip coefficient every data-
+// parallel replica derives from it must be bit-identical, or the replicas' weights drift apart):
+// pass 1, at most SQ_NORM_BLOCKS workgroups with 16-B loads, writes one partial per workgroup (each
+// thread's elements are fixed by its index and the grid, the grid by the sizes); pass 2, one
+// workgroup, folds the partials in index order into out[0]. Round 5 ended pass 1 with one f32
+// atomicAdd per workgroup on out[0]: an arrival-order sum that differed by ulps from launch to launch.
+constexpr int SQ_NORM_BLOCKS = COMET_SQ_NORM_PARTIALS;
+__global__ void __launch_bounds__(256) sq_norm_part_kernel(MultiPtr mp, float* __restrict__ part) {
   __shared__ float scratch[4];
   float s = 0.f;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -195,7 +199,15 @@ __global__ void sq_norm_kernel(MultiPtr mp, float* __restrict__ out) {
     for (int64_t i = head + nv * 4 + tid; i < n; i += stride) s += x[i] * x[i];
   }
   s = block_sum<4>(s, scratch);
-  if (threadIdx.x == 0) atomicAdd(out, s);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) sq_norm_fold_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float scratch[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) s += part[i];
+  s = block_sum<4>(s, scratch);
+  if (threadIdx.x == 0) out[0] += s;
 }
 
 // torch.optim.AdamW (foreach=False semantics): p *= 1 - lr*wd; m.lerp_(g, 1-b1);
@@ -410,8 +422,8 @@ extern "C" int comet_colsum(int dtype, const void* x, float* out, int64_t rows, 
 }
 
 extern "C" int comet_sq_norm_multi(const float* const* ptrs, const int64_t* sizes, int n_tensors,
-                                   float* out, void* stream) {
-  COMET_CHECK_ARG(out && n_tensors >= 0, "comet_sq_norm_multi: bad args");
+                                   float* out, float* partials, void* stream) {
+  COMET_CHECK_ARG(out && partials && n_tensors >= 0, "comet_sq_norm_multi: bad args");
   hipStream_t s = as_stream(stream);
   for (int base = 0; base < n_tensors; base += MT_MAX) {
     MultiPtr mp{};
@@ -424,8 +436,10 @@ extern "C" int comet_sq_norm_multi(const float* const* ptrs, const int64_t* size
     }
     int64_t g = cdiv(total / 4 + 1, 256);
     if (g > SQ_NORM_BLOCKS) g = SQ_NORM_BLOCKS;
-    hipLaunchKernelGGL(sq_norm_kernel, dim3((unsigned)g), dim3(256), 0, s, mp, out);
-    COMET_CHECK_LAUNCH("comet_sq_norm_multi");
+    hipLaunchKernelGGL(sq_norm_part_kernel, dim3((unsigned)g), dim3(256), 0, s, mp, partials);
+    COMET_CHECK_LAUNCH("comet_sq_norm_multi (partials)");
+    hipLaunchKernelGGL(sq_norm_fold_kernel, dim3(1), dim3(256), 0, s, (const float*)partials, (int)g, out);
+    COMET_CHECK_LAUNCH("comet_sq_norm_multi (fold)");
   }
   return COMET_OK;
 }
@@ -467,8 +481,204 @@ __global__ void __launch_bounds__(256) nonfinite_kernel(const T* __restrict__ x,
   c = (int)wave_sum((float)c);
   if ((threadIdx.x & 63) == 0 && c != 0) atomicAdd(count, c);
 }
+
+// LDS integrity probe (comet_lds_probe): the whole 160 KiB, one workgroup per CU. The pattern of
+// word i in round r of workgroup b is a hash of (b, r, i), so a word written by anything else --
+// or left over from another round -- is counted.
+constexpr int PROBE_WORDS = 160 * 1024 / 4;
+__device__ __forceinline__ unsigned probe_word(unsigned b, unsigned r, unsigned i) {
+  unsigned h = (b * 0x9E3779B1u) ^ (r * 0x85EBCA77u) ^ (i * 0xC2B2AE3Du);
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  return h ^ (h >> 12);
+}
+__global__ void __launch_bounds__(256) lds_probe_kernel(int rounds, int spin, uint32_t* __restrict__ bad) {
+  __shared__ unsigned lds[PROBE_WORDS];
+  unsigned miss = 0;
+  for (int r = 0; r < rounds; ++r) {
+    for (int i = threadIdx.x; i < PROBE_WORDS; i += 256) lds[i] = probe_word(blockIdx.x, r, i);
+    __syncthreads();
+    for (int k = 0; k < spin; ++k) __builtin_amdgcn_s_sleep(127);
+    for (int i = threadIdx.x; i < PROBE_WORDS; i += 256) miss += lds[i] != probe_word(blockIdx.x, r, i);
+    __syncthreads();
+  }
+  miss = (unsigned)wave_sum((float)miss);
+  if ((threadIdx.x & 63) == 0 && miss != 0) atomicAdd(bad, miss);
+}
+
+// Cross-lane exchange probe (comet_shfl_probe): every wave reduces known integers over its 64 lanes
+// `iters` times and counts lanes whose result is wrong. mode 0: xor butterfly by __shfl_xor
+// (ds_bpermute_b32, through the LDS crossbar); mode 1: the same sums by DPP row_mirror /
+// row_half_mirror / quad_perm steps and v_permlane16_swap / v_permlane32_swap (VALU only);
+// mode 2: through the wave's own LDS words (ds_write_b32, ds_read_b32 of the xor-16 partner).
+__global__ void __launch_bounds__(256) shfl_probe_kernel(int iters, int mode, uint32_t* __restrict__ bad) {
+  __shared__ int ex[256];
+  const int lane = threadIdx.x & 63;
+  unsigned miss = 0;
+  for (int it = 0; it < iters; ++it) {
+    const int v = lane * 7 + it + (int)blockIdx.x;
+    const int want = 7 * 2016 + 64 * (it + (int)blockIdx.x);
+    int x = v;
+    if (mode == 0) {
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    } else if (mode == 1) {
+      x += __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false);  // row_mirror
+      x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+      x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+      x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+      const auto w16 = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+      x = (int)(w16[0] + w16[1]);
+      const auto w32 = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+      x = (int)(w32[0] + w32[1]);
+    } else if (mode == 3 || mode == 4) {
+      // two sums reduced together (the row-LN statistics' shape): small integers as f32, so every
+      // order of the adds gives the same exact value; mode 3 lets hipcc pair the adds into
+      // v_pk_add_f32, mode 4 keeps them scalar (an empty asm between the two)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      float a = (float)v, b = (float)(2 * v + 1);
+      if (mode == 3) {
+        f2 p = {a, b};
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+          const f2 q = {__shfl_xor(p.x, m, 64), __shfl_xor(p.y, m, 64)};
+          p += q;  // v_pk_add_f32
+        }
+        a = p.x;
+        b = p.y;
+      } else {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+          const float pa = __shfl_xor(a, m, 64), pb = __shfl_xor(b, m, 64);
+          a += pa;
+          asm volatile("" : "+v"(a));
+          b += pb;
+        }
+      }
+      const bool ok = a == (float)want && b == (float)(2 * want + 64);
+      x = ok ? want : want + 1;
+    } else if (mode == 5 || mode == 6) {
+      // one VOP3P instruction, 32 times: mode 5 the row-LN reduce's centring form (op_sel: the low
+      // result reads the high half of the second pair; op_sel_hi: the high result its low half;
+      // both negated), mode 6 the plain form; small integers, so the results are exact
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 a = {(float)v, (float)(v + 3)};
+      int okc = 0;
+#pragma unroll 4
+      for (int u = 0; u < 32; ++u) {
+        const f2 b = {(float)(u + lane), (float)(2 * u - lane)};
+        f2 r;
+        if (mode == 5) {
+          asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]"
+                       : "=v"(r) : "v"(a), "v"(b));
+          okc += r.x == a.x - b.y && r.y == a.y - b.x;
+        } else {
+          asm volatile("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+          okc += r.x == a.x - b.x && r.y == a.y - b.y;
+        }
+      }
+      x = okc == 32 ? want : want + 1;
+    } else if (mode >= 7 && mode <= 11) {
+      // which VOP3P form: 7 op_sel:[0,1] alone, 8 op_sel_hi:[1,0] alone, 9 v_pk_mul_f32 op_sel:[0,1],
+      // 10 v_pk_fma_f32 op_sel:[0,1,0], 11 v_pk_add_f32 op_sel:[1,0] (the first source's high half)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 a = {(float)v, (float)(v + 3)};
+      int okc = 0;
+#pragma unroll 4
+      for (int u = 0; u < 32; ++u) {
+        const f2 b = {(float)(u + lane), (float)(2 * u - lane)};
+        f2 r;
+        bool ok;
+        if (mode == 7) {
+          asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == a.x + b.y && r.y == a.y + b.y;
+        } else if (mode == 8) {
+          asm volatile("v_pk_add_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == a.x + b.x && r.y == a.y + b.x;
+        } else if (mode == 9) {
+          asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == a.x * b.y && r.y == a.y * b.y;
+        } else if (mode == 10) {
+          asm volatile("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[0,1,0]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == fmaf(a.x, b.y, a.x) && r.y == fmaf(a.y, b.y, a.y);
+        } else {
+          asm volatile("v_pk_add_f32 %0, %1, %2 op_sel:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == a.y + b.x && r.y == a.y + b.y;
+        }
+        okc += ok;
+      }
+      x = okc == 32 ? want : want + 1;
+    } else if (mode >= 13 && mode <= 16) {
+      // 13-15: v_pk_mov_b32 op_sel:[1,0] / [0,1] / [1,1] (dst.lo = src0[op_sel0], dst.hi =
+      // src1[op_sel1]); 16: v_pk_fma_f32 op_sel:[0,0,1] (the addend's high half into the low result)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const f2 a = {(float)v, (float)(v + 3)};
+      int okc = 0;
+#pragma unroll 4
+      for (int u = 0; u < 32; ++u) {
+        const f2 b = {(float)(u + lane), (float)(2 * u - lane)};
+        f2 r;
+        bool ok;
+        if (mode == 13) {
+          asm volatile("v_pk_mov_b32 %0, %1, %2 op_sel:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == a.y && r.y == b.x;
+        } else if (mode == 14) {
+          asm volatile("v_pk_mov_b32 %0, %1, %2 op_sel:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == a.x && r.y == b.y;
+        } else if (mode == 15) {
+          asm volatile("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == a.y && r.y == b.y;
+        } else {
+          asm volatile("v_pk_fma_f32 %0, %1, %1, %2 op_sel:[0,0,1]" : "=v"(r) : "v"(a), "v"(b));
+          ok = r.x == fmaf(a.x, a.x, b.y) && r.y == fmaf(a.y, a.y, b.y);
+        }
+        okc += ok;
+      }
+      x = okc == 32 ? want : want + 1;
+    } else if (mode == 12) {
+      // aggressor: a back-to-back MFMA stream (16x16x32 bf16), nothing checked
+      typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      const b8 fa = __builtin_bit_cast(b8, uint4{(unsigned)v, 2u, 3u, 4u});
+      f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0, acc2 = acc0, acc3 = acc0;
+#pragma unroll 4
+      for (int u = 0; u < 64; ++u) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fa, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fa, acc1, 0, 0, 0);
+        acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fa, acc2, 0, 0, 0);
+        acc3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fa, acc3, 0, 0, 0);
+      }
+      x = (acc0[0] + acc1[1] + acc2[2] + acc3[3]) == 12345.f ? want + 1 : want;
+    } else {
+      ex[threadIdx.x] = v;
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's write is in LDS
+      const int p = ex[threadIdx.x ^ 16];
+      x = (v + p == 2 * v + ((lane ^ 16) - lane) * 7) ? want : want + 1;
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    miss += x != want;
+  }
+  miss = (unsigned)wave_sum((float)miss);
+  if (lane == 0 && miss != 0) atomicAdd(bad, miss);
+}
 }  // namespace
 }  // namespace comet
+
+extern "C" int comet_shfl_probe(int groups, int iters, int mode, uint32_t* bad, void* stream) {
+  using namespace comet;
+  COMET_CHECK_ARG(bad != nullptr && groups > 0 && iters > 0 && mode >= 0 && mode <= 16, "comet_shfl_probe: bad args");
+  hipLaunchKernelGGL(shfl_probe_kernel, dim3((unsigned)groups), dim3(256), 0, as_stream(stream), iters, mode, bad);
+  COMET_CHECK_LAUNCH("comet_shfl_probe");
+  return COMET_OK;
+}
+
+extern "C" int comet_lds_probe(int groups, int rounds, int spin, uint32_t* bad, void* stream) {
+  using namespace comet;
+  COMET_CHECK_ARG(bad != nullptr && groups > 0 && rounds > 0 && spin >= 0 && spin <= 1024, "comet_lds_probe: bad args");
+  hipLaunchKernelGGL(lds_probe_kernel, dim3((unsigned)groups), dim3(256), 0, as_stream(stream), rounds, spin, bad);
+  COMET_CHECK_LAUNCH("comet_lds_probe");
+  return COMET_OK;
+}
 
 extern "C" int comet_count_nonfinite(int dtype, const void* x, int64_t n, int32_t* count, void* stream) {
   using namespace comet;

@@ -1938,10 +1938,14 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     if (!tile_end) continue;
     tile_epilogue(q / nk, q, qa1);
   }
-  }
-#ifdef COMET_GEMM_STAMPS
+  // The k-tile stream runs two k-tiles past the last one (re-loads nothing reads), so up to two
+  // batches of LDS-DMA pieces can still be in flight here when the last epilogue issued no load of
+  // its own (bf16 outputs of a Linear without bias: the tracker's q / kv projections). Drained so
+  // no workgroup ends with LDS writes pending (round 6: comet_lds_probe workgroups placed on a CU as
+  // these leave saw no late write with or without this wait, tools/lds_race.py; one wait per
+  // workgroup and kernel, kept as the guarantee)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
+  }
 }
 }  // namespace w4
 
@@ -2174,8 +2178,8 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   // (profiles/r05_n: 8192^3 +8..14 %, M 74368 N 2304 K 768 +4 %, the f32 + residual K 3072 shape
   // +1..2 %; with GELU at K 768 even, K <= 384 5-9 % slower -- the tile's two wave groups then run
   // their epilogues one after the other and drain the stores once per tile). COMET_GEMM_PING=1 / =0
-  // forces it on / off (measurement).
-  static const char* ping_env = getenv("COMET_GEMM_PING");
+  // forces it on / off (measurement; read per call, so one test process can run both loops).
+  const char* ping_env = getenv("COMET_GEMM_PING");
   const bool ping = ping_env != nullptr ? ping_env[0] == '1'
                                         : (a.aux == nullptr && a.act == COMET_ACT_NONE &&
                                            ((a.k >= 768 && a.dtype_c == COMET_BF16 && a.resid == nullptr) ||
@@ -2951,10 +2955,14 @@ static bool rowln_ok(const comet_gemm_args& a, const comet_rowln_args* ln) {
   int tbm, tbn;
   pp_tile_base(a, tbm, tbn);
   if (tbn != a.n) return false;
+  // the epilogues (persistent and split reduce) read bias / zw / zb as f32x4 per 4 columns
+  auto a16 = [](const void* p) { return p == nullptr || (uintptr_t)p % 16 == 0; };
+  if (!a16(a.bias)) return false;
   if (ln == nullptr) return true;
   auto b4 = [](const void* p, int64_t ld) { return p == nullptr || ((uintptr_t)p % 8 == 0 && ld % 4 == 0); };
   if (!b4(ln->y16, ln->ldy) || !b4(ln->z16, ln->ldz)) return false;
   if (ln->z16 != nullptr && (ln->zw == nullptr || ln->zb == nullptr)) return false;
+  if (!a16(ln->zw) || !a16(ln->zb)) return false;
   return true;
 }
 

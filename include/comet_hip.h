@@ -257,9 +257,12 @@ int comet_colsum(int dtype, const void* x, float* out, int64_t rows, int64_t col
 int comet_act_bwd_colsum(int act, int dtype_pre, const void* pre, int dtype_dy, const void* dy,
                          int dtype_out, void* out, float* dbias, int64_t rows, int64_t cols,
                          int accumulate, void* stream);
-/* squared L2 norm of many tensors: out[0] += sum x_i^2  (clip_grad_norm_, train_eval_func_new_cp5.py:797) */
+/* squared L2 norm of many tensors: out[0] += sum x_i^2  (clip_grad_norm_, train_eval_func_new_cp5.py:797),
+ * in a fixed summation order (bit-identical across launches: the clip coefficient of every
+ * data-parallel replica); partials: device scratch of COMET_SQ_NORM_PARTIALS floats, stream-ordered. */
+#define COMET_SQ_NORM_PARTIALS 1024
 int comet_sq_norm_multi(const float* const* ptrs, const int64_t* sizes, int n_tensors,
-                        float* out, void* stream);
+                        float* out, float* partials, void* stream);
 /* fused AdamW over many f32 tensors (torch.optim.AdamW defaults, train_util.py:311-332);
  * grad scaled by clip = min(1, max_norm / (sqrt(*sqnorm) + 1e-6)) when sqnorm != NULL. */
 int comet_adamw_multi(float* const* params, const float* const* grads, float* const* exp_avg,
@@ -466,6 +469,18 @@ int comet_maxfilt2d(const float* x, float* y, float* tmp, int B, int H, int W, i
  *   -1. */
 int comet_count_nonfinite(int dtype, const void* x, int64_t n, int32_t* count, void* stream);
 int comet_debug_flags(int clear);
+/* comet_lds_probe: LDS integrity probe for concurrency tests (tools/lds_race.py,
+ *   tests/test_ops_gpu.py). `groups` workgroups each own the CU's whole LDS (160 KiB): per round
+ *   they fill it with a pattern keyed by (workgroup, round), sleep about `spin` x 8k cycles and
+ *   count the words that changed, adding the count to *bad (a uint32 on the device). A workgroup's
+ *   LDS is its own, so any change is a write that landed after the CU handed the LDS over -- e.g.
+ *   LDS-DMA of a kernel that ended with pieces in flight. */
+int comet_lds_probe(int groups, int rounds, int spin, uint32_t* bad, void* stream);
+/* comet_shfl_probe: cross-lane exchange probe for concurrency tests (tools/op_repeat.py). Each wave
+ *   sums known integers over its 64 lanes `iters` times -- mode 0 by ds_bpermute (__shfl_xor), 1 by
+ *   DPP + v_permlane swaps, 2 through its own LDS words -- and adds the number of wrong lane results
+ *   to *bad (uint32 on the device). */
+int comet_shfl_probe(int groups, int iters, int mode, uint32_t* bad, void* stream);
 
 #ifdef __cplusplus
 }

@@ -36,3 +36,16 @@ def test_error_path_reports_message():
     rc = lib.comet_gemm(ctypes.byref(g), None)
     assert rc == -1
     assert b"layout" in lib.comet_last_error() or b"batch" in lib.comet_last_error()
+
+
+def test_library_has_no_packed_fp32_high_src1_reads():
+    """The built library holds no packed-FP32 VOP3P instruction whose low result reads the high dword
+    of its second / third source (op_sel:[x,1,..]): on gfx950 those return wrong values beside a
+    co-resident MFMA wave (round 6, tools/isa_hazard.py; the Makefile builds with
+    -fno-slp-vectorize). The probe kernel that reproduces the hazard on purpose is exempt."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_hazard
+    bad = isa_hazard.check()
+    assert not bad, {k[:80]: len(v) for k, v in bad.items()}

@@ -234,7 +234,8 @@ def test_batch_shard_partitions_batches():
 
 
 def test_batch_shard_even_batches_cycles_from_start():
-    """even_batches=True, drop_last=False (accelerate's default, train_e2epose2.py): 23 samples in
+    """even_batches=True, drop_last=False (accelerate's default; the reference's entry points pass
+    even_batches=False, train_e2epose2.py:47 -- this pins the default path of _BatchShard): 23 samples in
     batches of 2 (the last one short) over 4 ranks -> 3 full batches per rank; the short batch is
     completed and the round filled with indices cycled from the start of the epoch."""
     from comet_amd.loop import _BatchShard
