@@ -1949,6 +1949,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
 }
 }  // namespace w4
 
+
 int g_num_cus = 0;
 int num_cus() {
   if (g_num_cus == 0) {
@@ -2234,7 +2235,7 @@ int big_bn(const comet_gemm_args& a) {
 
 struct Plan {
   int kind;      // 0 skinny, 1 256-row tile, 2 128 x 128 tile, 3 persistent tile kernel,
-                 // 4 two-workgroups-per-CU 256 x 128 kernel (gemm_w2.hip, opt-in)
+                 // 4 two-workgroups-per-CU 256 x 128 kernel (removed)
   int bn;        // kind 1, 3: column tile
   int splits;    // requested K splits (before the workspace check)
   int bm = 0;    // kind 3: row tile

@@ -24,6 +24,8 @@ SHAPES = [  # (M, N, K, act, out dtype, residual)  -- profiles/r02_v3/gemm_shape
     (65536, 1024, 256, L.ACT_GELU, torch.bfloat16, False),
     (65536, 768, 256, L.ACT_NONE, torch.bfloat16, False),
     (74368, 3072, 768, L.ACT_GELU, torch.bfloat16, False),
+    (65536, 1536, 384, L.ACT_NONE, torch.bfloat16, False),  # the GELU shapes without the activation:
+    (74368, 3072, 768, L.ACT_NONE, torch.bfloat16, False),  # the epilogue's share
     (74368, 2304, 768, L.ACT_NONE, torch.bfloat16, False),
     (74368, 768, 3072, L.ACT_NONE, torch.float32, True),
     (74368, 768, 768, L.ACT_NONE, torch.float32, True),
