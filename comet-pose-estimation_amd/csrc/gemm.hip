@@ -43,6 +43,7 @@ struct Epi {
   int wide = 0;  // persistent kernel: 16-B bf16 stores (C 16-B aligned, ldc % 8 == 0; host-checked)
   int prio = 0;  // persistent kernel: s_setprio 1 for waves 4-7 (COMET_GEMM_PRIO=1, measurement)
   int bpark = 0;  // persistent kernel: bf16-park epilogue (COMET_GEMM_NO_BPARK=1: the direct / f32-park paths)
+  int raster = 0;  // persistent kernel: per-XCD contiguous tile ranges (COMET_GEMM_RASTER=1, measurement)
   // 256-row kernel, DACT instances (comet_gemm_dact): C = act'(pre) * acc with pre [M, N] bf16 at
   // row pitch ldg, and dcol[n] += sum over rows of the stored (rounded) values
   const __bf16* gpre = nullptr; int64_t ldg = 0; float* dcol = nullptr;
@@ -1139,8 +1140,18 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   const int G = gridDim.x, bid = blockIdx.x;
   const int tiles_m = ntiles / tiles_n;
   const bool single = ntiles <= G;
-  const int off = single ? xcd_remap(bid, G) : (bid & 7) * (G >> 3) + (bid >> 3);
-  const int my_tiles = single ? 1 : (off < ntiles ? (ntiles - off + G - 1) / G : 0);
+  // tile it of this workgroup is logical tile off + it * strd, below lim. Default: wave it of the
+  // grid takes logical tiles [it * G, (it + 1) * G), XCD x (= bid & 7) the x-th 32 of them. With
+  // epi.raster (COMET_GEMM_RASTER=1, measurement) each XCD walks its own contiguous eighth of the
+  // logical tiles instead, so an A row block is fetched into at most two XCDs' L2.
+  int off = single ? xcd_remap(bid, G) : (bid & 7) * (G >> 3) + (bid >> 3), strd = G, lim = ntiles;
+  if (!single && epi.raster && (G & 7) == 0) {
+    const int x = bid & 7, per = ntiles >> 3, rem = ntiles & 7, base = x * per + min(x, rem);
+    lim = base + per + (x < rem ? 1 : 0);
+    off = base + (bid >> 3);
+    strd = G >> 3;
+  }
+  const int my_tiles = single ? 1 : (off < lim ? (lim - off + strd - 1) / strd : 0);
   const int T = my_tiles * nk;
   if (T == 0) return;
 
@@ -1166,7 +1177,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   auto lch = [&](int r) { return ((lane & 7) ^ ((r >> 1) & 7)) * 8; };
   auto set_tile_a = [&](int it) {
     int tm, tn;
-    tile_rc(off + it * G, tiles_m, tiles_n, tm, tn);
+    tile_rc(off + it * strd, tiles_m, tiles_n, tm, tn);
     const int m0 = tm * TBM;
     ldA = A + (int64_t)m0 * lda;
 #pragma unroll
@@ -1175,7 +1186,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
   };
   auto set_tile_b = [&](int it) {
     int tm, tn;
-    tile_rc(off + it * G, tiles_m, tiles_n, tm, tn);
+    tile_rc(off + it * strd, tiles_m, tiles_n, tm, tn);
     const int n0 = tn * TBN;
     ldB = B + (int64_t)n0 * ldb;
 #pragma unroll
@@ -1264,7 +1275,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
       // ---- epilogue of the tile, straight from the accumulators: lane (li, g) of fragment
       // (i, j) holds C[row0 + i*16 + li][col0 + j*16 + 4g + r], r = 0..3
       int tm, tn;
-      tile_rc(off + tix * G, tiles_m, tiles_n, tm, tn);
+      tile_rc(off + tix * strd, tiles_m, tiles_n, tm, tn);
       const int64_t row0 = (int64_t)tm * TBM + wr * WROWS + li;
       const int64_t col0 = (int64_t)tn * TBN + wc * WCOLS + 4 * g;
       const TC* R = reinterpret_cast<const TC*>(epi.resid);
@@ -1736,7 +1747,7 @@ gemm_w4_kernel(const __bf16* __restrict__ A, int64_t lda, const __bf16* __restri
     int oA[2], oB[2];
     auto pset = [&](int it) {
       int tm, tn;
-      tile_rc(off + it * G, tiles_m, tiles_n, tm, tn);
+      tile_rc(off + it * strd, tiles_m, tiles_n, tm, tn);
       const int m0 = tm * TBM, n0 = tn * TBN;
       sA = A + (int64_t)m0 * lda;
       sB = B + (int64_t)n0 * ldb;
@@ -2126,6 +2137,7 @@ int launch_pp_rowln(const comet_gemm_args& a, const w4::RowLN& ln, hipStream_t s
   }
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, nullptr, 0, 0, 0, a.alpha, COMET_ACT_NONE, 1};
   e.prio = getenv("COMET_GEMM_PRIO") != nullptr;
+  e.raster = getenv("COMET_GEMM_RASTER") != nullptr && getenv("COMET_GEMM_RASTER")[0] == '1';
   int grid = num_cus();
   grid -= grid % 8;
   int tbm, tbn;
@@ -2160,6 +2172,10 @@ int launch_pp(const comet_gemm_args& a, hipStream_t s) {
   Epi e{a.bias, a.bias_mode, 0, 0, a.resid, a.ldr, 0, 0, a.beta, a.aux, a.ldaux, 0, 0, a.alpha, a.act, 1};
   e.wide = (uintptr_t)a.c % 16 == 0 && a.ldc % 8 == 0 && getenv("COMET_GEMM_NO_WIDE") == nullptr;
   e.prio = getenv("COMET_GEMM_PRIO") != nullptr;
+  // per-XCD contiguous tile ranges: measurement only (COMET_GEMM_RASTER=1). Alone, 4-5 % faster on the
+  // K = 768 shapes and 1-6 % slower at K 384 / 3072, with 22 % more L2 fill traffic; as the default
+  // for K 512..1024 the step measured 0.1 ms slower (tools/raster_ab.py, profiles/r06_raster)
+  e.raster = getenv("COMET_GEMM_RASTER") != nullptr && getenv("COMET_GEMM_RASTER")[0] == '1';
   e.bpark = (uintptr_t)a.c % 16 == 0 && a.ldc % 8 == 0 && (a.aux == nullptr || ((uintptr_t)a.aux % 16 == 0 && a.ldaux % 8 == 0)) &&
             getenv("COMET_GEMM_NO_BPARK") == nullptr;
   const w4::RowLN noln{};

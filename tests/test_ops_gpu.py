@@ -1114,6 +1114,42 @@ def test_gemm_ping_pong_path(mnk, epi, ping, monkeypatch):
     assert bad == 0, f"{epi} {mnk} ping={ping}: max err {err.max().item():.3e}, {bad} bad"
 
 
+@pytest.mark.parametrize("mnk", [(74368 + 40, 2304 + 16, 768), (20000, 1000, 768), (65536, 1152, 384),
+                                 (9000, 768, 1024), (33000, 768, 3072)])
+@pytest.mark.parametrize("odt", ["bf16_gelu", "f32_resid"])
+def test_gemm_tile_order(mnk, odt, monkeypatch):
+    """The persistent kernel's two tile orders (gemm.hip: XCD-banded waves, the default, and per-XCD
+    contiguous tile ranges, COMET_GEMM_RASTER=1, a measurement switch) compute every tile the same
+    way: bit-identical outputs, within the f64 bound, on tiled shapes with M / N tails and tile counts
+    that do not divide by the 8 XCDs (modules.py:119-154 Linear)."""
+    ops = _ops()
+    M, N, K = mnk
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    xd = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+    wd = (torch.randn(N, K, device=DEV, generator=g) * K ** -0.5).to(torch.bfloat16)
+    bd = torch.randn(N, device=DEV, generator=g)
+    rd = torch.randn(M, N, device=DEV, generator=g) if odt == "f32_resid" else None
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("COMET_GEMM_RASTER", mode)
+        if rd is None:
+            outs[mode] = ops.linear(xd, wd, bias=bd, act=1, out_dtype=torch.bfloat16)
+        else:
+            outs[mode] = ops.linear(xd, wd, bias=bd, resid=rd, out_dtype=torch.float32)
+        assert ops._PLAN[0] == 3, f"expected the persistent plan, got {tuple(ops._PLAN)}"
+    assert torch.equal(outs["0"], outs["1"]), f"{mnk} {odt}: the tile order changed the result"
+    pre = xd.double() @ wd.double().t() + bd.double()
+    if rd is None:
+        ref = torch.nn.functional.gelu(pre)
+        tol = 1e-2 * ref.abs() + 1e-2
+    else:
+        ref = pre + rd.double()
+        tol = 1e-4 * ref.abs() + 2e-5 * math.sqrt(K)
+    err = (outs["1"].double() - ref).abs()
+    bad = int((err > tol).sum())
+    assert bad == 0, f"{mnk} {odt}: max err {err.max().item():.3e}, {bad} bad"
+
+
 def test_cast_multi_and_weight_cache_refresh():
     """comet_cast_multi_f32_bf16 equals torch's RNE .to(bfloat16) bit for bit (aligned and
     unaligned views, > 48 tensors); refresh_weight_cache re-casts cached copies in place after

@@ -18,6 +18,8 @@
 #   smoke             __graft_entry__.smoke()
 #   bench[:args]      python bench.py [args] -> bench*.json
 #   prof              rocprofv3 kernel-trace statistics of the bench step
+#   py:<cmd+args>     python <cmd args> alone (words joined by '+'; leading VAR=V words -> env)
+#   pmcg:<M+N+K+act+dt+res>[@VAR=V]  FETCH_SIZE and WRITE_SIZE passes (one each) over tools/gemm_one.py
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -138,6 +140,22 @@ for s in "$@"; do
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $O/prof -o run -- python bench.py --no-cpu-baseline \
         --steps 5 --warmup 2 > $O/bench_prof.json 2> $O/bench_prof.err || fail $? "$s" ;;
+    py:*)
+      cmd=$(echo ${s#py:} | tr '+' ' ')
+      tagp=$(echo ${s#py:} | tr '+/.=' '____' | cut -c1-80)
+      e=""; while [[ $cmd == *=* && ${cmd%% *} == *=* ]]; do e="$e ${cmd%% *}"; cmd=${cmd#* }; done
+      env X=1 $e timeout -k 10 300 python -u $cmd > $O/$tagp.txt 2>&1 || { tail -20 $O/$tagp.txt; fail $? "$s"; }
+      grep -v amdgpu.ids $O/$tagp.txt | tail -40 ;;
+    pmcg:*)
+      spec=${s#pmcg:}
+      shp=$(echo ${spec%@*} | tr '+' ' ')
+      e="X=1"; [[ $spec == *@* ]] && e=$(echo ${spec#*@} | tr ',' ' ')
+      tagp=pmcg_$(echo "$spec" | tr '+@=,' '____')
+      for c in FETCH_SIZE WRITE_SIZE; do
+        env $e timeout -s KILL 90 rocprofv3 --pmc $c --kernel-trace --stats -f csv -d $O/$tagp/$c -o run -- python tools/gemm_one.py $shp 10 \
+          > $O/${tagp}_$c.log 2>&1 || { tail $O/${tagp}_$c.log; fail $? "$s $c"; }
+      done
+      python tools/pmc_kernel.py $O/$tagp comet_gemm ;;
     *) fail 2 "unknown step $s" ;;
   esac
 done
