@@ -142,7 +142,7 @@ for s in "$@"; do
         --steps 5 --warmup 2 > $O/bench_prof.json 2> $O/bench_prof.err || fail $? "$s" ;;
     py:*)
       cmd=$(echo ${s#py:} | tr '+' ' ')
-      tagp=$(echo ${s#py:} | tr '+/.=' '____' | cut -c1-80)
+      tagp=py${n}_$(echo ${s#py:} | tr '+/.=' '____' | rev | cut -c1-60 | rev)
       e=""; while [[ $cmd == *=* && ${cmd%% *} == *=* ]]; do e="$e ${cmd%% *}"; cmd=${cmd#* }; done
       env X=1 $e timeout -k 10 300 python -u $cmd > $O/$tagp.txt 2>&1 || { tail -20 $O/$tagp.txt; fail $? "$s"; }
       grep -v amdgpu.ids $O/$tagp.txt | tail -40 ;;
