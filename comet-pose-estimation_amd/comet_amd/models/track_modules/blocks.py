@@ -89,7 +89,8 @@ class ShallowEncoder(nn.Module):
     @torch.no_grad()
     def forward(self, x, with_pool=False):
         """x NHWC [n, P, P, 3] -> NHWC [n, P/stride, P/stride, 32] (with_pool: also its 2x2 average
-        pool, the fine correlation pyramid's level 1, written by the same up-sampling kernel)."""
+        pool, the fine correlation pyramid's level 1: conv2, the residual, the up-sampling and the
+        pool in one kernel, comet_conv1x1_resize_pool_nhwc)."""
         _, H, W, _ = x.shape
         x = ops.instnorm_nhwc(conv2d_nhwc(x, self.conv1, 2, 1), relu=True)
         h, w = x.shape[1], x.shape[2]
@@ -98,10 +99,15 @@ class ShallowEncoder(nn.Module):
         tmp = self.layer2(tmp)
         x = ops.resize_bilinear(tmp, h, w, nhwc=True, out=x, add=True)
         n, _, _, c = x.shape
-        x = F.linear(x.reshape(-1, c), F.wcast(self.conv2.weight.reshape(c, c)), self.conv2.bias,
-                     resid=x.reshape(-1, c), out_dtype=x.dtype).reshape(n, h, w, c)
         oh, ow = H // self.stride, W // self.stride
+        w2 = F.wcast(self.conv2.weight.reshape(c, c))
+        if with_pool and ops.conv1x1_resize_pool_ok(x, w2, self.conv2.bias):
+            # conv2 (1x1) + residual, up-sampling and the pyramid's pool in one kernel (t never in HBM)
+            return ops.conv1x1_resize_pool(x, w2, self.conv2.bias, oh, ow)
+        x = F.linear(x.reshape(-1, c), w2, self.conv2.bias, resid=x.reshape(-1, c), out_dtype=x.dtype).reshape(n, h, w, c)
         if with_pool:
+            if ops.resize_pool_ok(x):
+                return ops.resize_bilinear_pool(x, oh, ow)
             y = ops.resize_bilinear(x, oh, ow, nhwc=True)
             return y, ops.avgpool2_nhwc(y)
         return ops.resize_bilinear(x, oh, ow, nhwc=True)

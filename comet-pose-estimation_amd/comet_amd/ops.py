@@ -589,6 +589,45 @@ def cast_multi_f32_bf16(srcs, dsts):
     L.check(L.load().comet_cast_multi_f32_bf16(S, D, Z, n, stream()), "cast_multi")
 
 
+def resize_bilinear_pool(x, oh, ow):
+    """NHWC x [n, h, w, c] -> (y [n, oh, ow, c] bilinear, align_corners=True; its 2 x 2 average
+    pool [n, oh // 2, ow // 2, c]) in one kernel: resize_bilinear + avgpool2_nhwc bit for bit."""
+    n, h, w, c = x.shape
+    xc = x.contiguous()
+    y = torch.empty(n, oh, ow, c, device=x.device, dtype=x.dtype)
+    p = torch.empty(n, oh // 2, ow // 2, c, device=x.device, dtype=x.dtype)
+    L.check(L.load().comet_resize_bilinear_pool_nhwc(dt(xc), dt(y), _p(xc), _p(y), _p(p), n, c, h, w, oh, ow,
+                                                     stream()), "resize_bilinear_pool")
+    return y, p
+
+
+def conv1x1_resize_pool(x, w, b, oh, ow):
+    """NHWC bf16 x [n, h, w, c]: t = x + x W^T + b (W [c, c] bf16, b f32), y = resize(t) to
+    [n, oh, ow, c], pool = avgpool2(y), in one kernel: linear(resid=x) + resize_bilinear_pool bit for
+    bit, without t in HBM (the fine ShallowEncoder's conv2 + up-sampling, blocks.py:105-110)."""
+    n, h, ww, c = x.shape
+    y = torch.empty(n, oh, ow, c, device=x.device, dtype=x.dtype)
+    p = torch.empty(n, oh // 2, ow // 2, c, device=x.device, dtype=x.dtype)
+    L.check(L.load().comet_conv1x1_resize_pool_nhwc(_p(x), _p(w), _p(b), _p(y), _p(p), n, c, h, ww, oh, ow,
+                                                    stream()), "conv1x1_resize_pool")
+    return y, p
+
+
+def conv1x1_resize_pool_ok(x, w, b):
+    n, h, ww, c = x.shape
+    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and c in (32, 64) and x.is_contiguous()
+            and w.is_contiguous() and tuple(w.shape) == (c, c) and (h * ww) % 16 == 0 and 4 * h * ww * c <= 65536
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and (b is None or (b.dtype == torch.float32 and b.is_contiguous())))
+
+
+def resize_pool_ok(x):
+    """comet_resize_bilinear_pool_nhwc's conditions (c % 8, 16-B alignment, input image <= 32 KiB)."""
+    n, h, w, c = x.shape
+    return (x.is_contiguous() and c in (8, 16, 32, 64, 128, 256) and x.data_ptr() % 16 == 0
+            and h * w * c * x.element_size() <= 32768)
+
+
 def resize_bilinear_into(x, out, add=False):
     """NHWC x [n, h, w, c] resized into out [n, oh, ow, c], a channel slice of a wider NHWC tensor
     (out.stride() == (oh*ow*ld, ow*ld, ld, 1))."""
@@ -941,7 +980,7 @@ def _timed(fn):
 
 
 for _name in ("layernorm", "layernorm_bwd", "layernorm_bwd_res", "cast", "cast_multi_f32_bf16", "act_bwd", "colsum",
-              "act_bwd_colsum", "instnorm_nhwc", "resize_bilinear", "resize_bilinear_into", "im2col_nhwc", "act_fwd",
+              "act_bwd_colsum", "instnorm_nhwc", "resize_bilinear", "resize_bilinear_into", "resize_bilinear_pool", "conv1x1_resize_pool", "im2col_nhwc", "act_fwd",
               "binary", "add_rows", "rowscale", "rowscale_bwd", "sample_bilinear", "corr_sample", "tracker_tokens",
               "coords_update", "avgpool2_nhwc", "patch_gather", "refine_combine", "track_score", "dino_prep",
               "pose_encode", "pose_decode", "pose_encode3", "pose_decode3", "images_nhwc", "harmonic_fwd",

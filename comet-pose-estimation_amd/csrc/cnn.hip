@@ -31,15 +31,24 @@ __global__ void im2col_nhwc_kernel(const TI* __restrict__ x, TO* __restrict__ co
   }
 }
 
-// align_corners=True bilinear: src = dst * (in-1)/(out-1)
+// align_corners=True bilinear: src = dst * (in-1)/(out-1). Contraction off here and in bilerp, so
+// every kernel that inlines them rounds each product and sum the same way (the fused resize + pool
+// kernel equals resize followed by avgpool2 bit for bit whatever hipcc fuses around it)
 __device__ __forceinline__ void ac_coord(int64_t o, int64_t in, int64_t out, int64_t& i0,
                                          int64_t& i1, float& f) {
+#pragma clang fp contract(off)
   const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
   const float src = scale * (float)o;
   i0 = (int64_t)src;
   if (i0 > in - 1) i0 = in - 1;
   i1 = i0 + 1 < in ? i0 + 1 : in - 1;
   f = src - (float)i0;
+}
+
+// same association as ATen's upsample_bilinear2d: h0lambda*(w0l*v00 + w1l*v01) + h1lambda*(...)
+__device__ __forceinline__ float bilerp(float v00, float v01, float v10, float v11, float fx, float fy) {
+#pragma clang fp contract(off)
+  return (1.f - fy) * ((1.f - fx) * v00 + fx * v01) + fy * ((1.f - fx) * v10 + fx * v11);
 }
 
 template <typename TI, typename TO>
@@ -59,8 +68,7 @@ __global__ void resize_kernel(const TI* __restrict__ x, TO* __restrict__ y, int 
                   : to_f32(x[((ni * c + ci) * h + yy) * w + xx]);
     };
     const float v00 = at(y0, x0), v01 = at(y0, x1), v10 = at(y1, x0), v11 = at(y1, x1);
-    // same association as ATen's upsample_bilinear2d: h0lambda*(w0l*v00 + w1l*v01) + h1lambda*(...)
-    const float v = (1.f - fy) * ((1.f - fx) * v00 + fx * v01) + fy * ((1.f - fx) * v10 + fx * v11);
+    const float v = bilerp(v00, v01, v10, v11, fx, fy);
     float out = v;
     if (add) out += to_f32(y[i]);
     y[i] = from_f32<TO>(out);
@@ -97,7 +105,7 @@ resize_nhwc8_kernel(const TI* __restrict__ x, TO* __restrict__ y, int64_t n, int
     if (add) load8(yo, o);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float v = (1.f - fy) * ((1.f - fx) * v00[e] + fx * v01[e]) + fy * ((1.f - fx) * v10[e] + fx * v11[e]);
+      const float v = bilerp(v00[e], v01[e], v10[e], v11[e], fx, fy);
       o[e] = add ? o[e] + v : v;
     }
     store8(yo, o);
@@ -135,7 +143,7 @@ resize_nhwc8_rows_kernel(const TI* __restrict__ x, TO* __restrict__ y, RowBlock 
     if (add) load8(yo, o);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float v = (1.f - fy) * ((1.f - fx) * v00[e] + fx * v01[e]) + fy * ((1.f - fx) * v10[e] + fx * v11[e]);
+      const float v = bilerp(v00[e], v01[e], v10[e], v11[e], fx, fy);
       o[e] = add ? o[e] + v : v;
     }
     store8(yo, o);
@@ -175,11 +183,152 @@ resize_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, int c, int
     if (add) load8(yo + (int64_t)it * 8, o);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float v = (1.f - fy) * ((1.f - fx) * v00[e] + fx * v01[e]) + fy * ((1.f - fx) * v10[e] + fx * v11[e]);
+      const float v = bilerp(v00[e], v01[e], v10[e], v11[e], fx, fy);
       o[e] = add ? o[e] + v : v;
     }
     store8(yo + (int64_t)it * 8, o);
   }
+}
+
+// resize_nhwc8_img_kernel with the 2 x 2 average pool of its output written by the same workgroup
+// (the fine ShallowEncoder's 31 x 31 maps and the fine correlation pyramid's level 1, refine_track.py
+// -> blocks.py:371 F.avg_pool2d(fmaps, 2, stride=2)). A lane owns one output column x (8 channels) of
+// a row pair (2 py, 2 py + 1): its two pixels are stored by consecutive lanes as contiguous runs, and
+// the pool value of columns (x, x + 1) is summed on the even lane from the stored (rounded) values,
+// the odd lane's two by a shuffle, in avgpool2_rows_kernel's order ((a + b) + c) + d -- so y and the
+// pool equal resize followed by avg_pool2d bit for bit without reading y back. A row pair's lanes
+// are padded to an even column count so a column pair never straddles a wave (64 % (2 * c / 8) == 0:
+// c in {8, 16, 32, 64, 128, 256}); the odd last row of y (floor pooling drops it) is written after.
+// (workgroup body) y / pool of image ni from the staged input image `img` in LDS
+template <typename TI, typename TO>
+__device__ __forceinline__ void resize_pool_body(const TI* img, TO* __restrict__ y, TO* __restrict__ pool, int64_t ni,
+                                                 int c, int h, int w, int oh, int ow) {
+  const int cg8 = c / 8, ph = oh / 2, pw = ow / 2;
+  const int rpi = ((ow + 1) / 2) * 2 * cg8;  // lanes per row pair (even column count)
+  const int lane = threadIdx.x & 63;
+  TO* yo = y + ni * oh * ow * c;
+  TO* po = pool + ni * ph * pw * c;
+  auto pixel = [&](int oy, int ox, int cg, float (&o)[8]) {
+    int64_t y0, y1, x0, x1;
+    float fy, fx;
+    ac_coord(oy, h, oh, y0, y1, fy);
+    ac_coord(ox, w, ow, x0, x1, fx);
+    float v00[8], v01[8], v10[8], v11[8];
+    load8(img + ((int)y0 * w + (int)x0) * c + cg * 8, v00);
+    load8(img + ((int)y0 * w + (int)x1) * c + cg * 8, v01);
+    load8(img + ((int)y1 * w + (int)x0) * c + cg * 8, v10);
+    load8(img + ((int)y1 * w + (int)x1) * c + cg * 8, v11);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = bilerp(v00[e], v01[e], v10[e], v11[e], fx, fy);
+  };
+  const int items = ph * rpi;
+  // whole waves per trip (the shuffles need every lane of the wave)
+  for (int it0 = threadIdx.x - lane; it0 < items; it0 += 256) {
+    const int it = it0 + lane;
+    const int py = it / rpi, r = it - py * rpi, ox = r / cg8, cg = r - ox * cg8;
+    const bool live = it < items && ox < ow;
+    float a[8], cq[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = cq[e] = 0.f;
+    if (live) {
+      pixel(2 * py, ox, cg, a);
+      pixel(2 * py + 1, ox, cg, cq);
+      store8(yo + ((int64_t)(2 * py) * ow + ox) * c + cg * 8, a);
+      store8(yo + ((int64_t)(2 * py + 1) * ow + ox) * c + cg * 8, cq);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // the values y holds
+        a[e] = to_f32(from_f32<TO>(a[e]));
+        cq[e] = to_f32(from_f32<TO>(cq[e]));
+      }
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float b = __shfl_down(a[e], cg8, 64), d = __shfl_down(cq[e], cg8, 64);
+      o[e] = (a[e] + b + cq[e] + d) * 0.25f;
+    }
+    if (live && (ox & 1) == 0 && ox / 2 < pw) store8(po + ((int64_t)py * pw + ox / 2) * c + cg * 8, o);
+  }
+  if (oh & 1) {  // the last row of y (no pool)
+    for (int it = threadIdx.x; it < ow * cg8; it += 256) {
+      const int ox = it / cg8, cg = it - ox * cg8;
+      float o[8];
+      pixel(oh - 1, ox, cg, o);
+      store8(yo + ((int64_t)(oh - 1) * ow + ox) * c + cg * 8, o);
+    }
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void __launch_bounds__(256)
+resize_pool_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, TO* __restrict__ pool, int c, int h,
+                             int w, int oh, int ow) {
+  extern __shared__ uint4 img_lds[];
+  const int64_t ni = blockIdx.x;
+  const int nvec = (int)((int64_t)h * w * c * (int)sizeof(TI) / 16);
+  const uint4* src = reinterpret_cast<const uint4*>(x + ni * h * w * c);
+  for (int i = threadIdx.x; i < nvec; i += 256) img_lds[i] = src[i];
+  __syncthreads();
+  resize_pool_body<TI, TO>(reinterpret_cast<const TI*>(img_lds), y, pool, ni, c, h, w, oh, ow);
+}
+
+// The fine ShallowEncoder's tail in one pass per patch (blocks.py:105-110 with refine_track's pool):
+// t = x + conv2(x) (1x1, C x C, bias; the skinny GEMM's MFMA and epilogue, bit for bit: same
+// instruction on the same operands; its epilogue at alpha = beta = 1 is two exact-product fmas, i.e. the
+// adds (acc + bias) + x, rounded to bf16), then
+// y = resize(t) and pool = avgpool2(y) as resize_pool_nhwc8_img_kernel. x, t stay in LDS: the [n, h, w,
+// C] conv2 output never reaches HBM (one 16.7M-row GEMM and its 3.2 GB of traffic per step less).
+// bf16, C = 32 x NT16 / 2 (NT16 16-column MFMA tiles, one 32-deep k step per 32 input channels).
+template <int NT16>
+__global__ void __launch_bounds__(256)
+conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ wt, const float* __restrict__ bias,
+                           __bf16* __restrict__ y, __bf16* __restrict__ pool, int h, int w, int oh, int ow) {
+  constexpr int C = NT16 * 16, KC = C / 32;
+  extern __shared__ uint4 img_lds[];
+  const int64_t ni = blockIdx.x;
+  const int hw = h * w;
+  const int nvec = hw * C * 2 / 16;
+  const uint4* src = reinterpret_cast<const uint4*>(x + ni * hw * C);
+  for (int i = threadIdx.x; i < nvec; i += 256) img_lds[i] = src[i];
+  const __bf16* xs = reinterpret_cast<const __bf16*>(img_lds);
+  __bf16* ts = reinterpret_cast<__bf16*>(img_lds + nvec);
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  bf16x8 bf[NT16][KC];
+#pragma unroll
+  for (int nt = 0; nt < NT16; ++nt)
+#pragma unroll
+    for (int k = 0; k < KC; ++k) bf[nt][k] = *reinterpret_cast<const bf16x8*>(wt + (nt * 16 + li) * C + 32 * k + 8 * g);
+  float b4[NT16][4];
+#pragma unroll
+  for (int nt = 0; nt < NT16; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b4[nt][r] = bias != nullptr ? bias[nt * 16 + 4 * g + r] : 0.f;
+  __syncthreads();
+  for (int m0 = wv * 16; m0 < hw; m0 += 64) {  // 16 pixels per wave step (hw % 16 == 0, host-checked)
+    const int m = m0 + li;
+    f32x4 acc[NT16];
+#pragma unroll
+    for (int nt = 0; nt < NT16; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(xs + m * C + 32 * k + 8 * g);
+#pragma unroll
+      for (int nt = 0; nt < NT16; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[nt][k], a, acc[nt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT16; ++nt) {
+      const int n0 = nt * 16 + 4 * g;
+      float rr[4], v[4];
+      load4(xs + m * C + n0, rr);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] + b4[nt][r];  // = fma(alpha = 1, acc, bias) exactly
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = rr[r] + v[r];  // = fma(beta = 1, resid, v) exactly
+      store4(ts + m * C + n0, v);
+    }
+  }
+  __syncthreads();
+  resize_pool_body<__bf16, __bf16>(ts, y, pool, ni, C, h, w, oh, ow);
 }
 
 inline unsigned g1d(int64_t n) {
@@ -259,6 +408,53 @@ extern "C" int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, cons
   else RS(__bf16, float);
 #undef RS
   COMET_CHECK_LAUNCH("comet_resize_bilinear");
+  return COMET_OK;
+}
+
+extern "C" int comet_resize_bilinear_pool_nhwc(int dtype_in, int dtype_out, const void* x, void* y, void* pool,
+                                               int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
+                                               void* stream) {
+  COMET_CHECK_ARG(x && y && pool && n > 0 && c > 0 && h > 0 && w > 0 && oh >= 2 && ow >= 2,
+                  "comet_resize_bilinear_pool_nhwc: bad args");
+  const int esz = dtype_in == COMET_F32 ? 4 : 2;
+  COMET_CHECK_ARG(c % 8 == 0 && c <= 256 && 64 % (2 * (c / 8)) == 0 &&
+                      ((uintptr_t)x | (uintptr_t)y | (uintptr_t)pool) % 16 == 0 && h * w * c * esz <= 32768 &&
+                      oh * ow * c < (1ll << 30) && n < (1ll << 31),
+                  "comet_resize_bilinear_pool_nhwc: needs c in {8, 16, 32, 64, 128, 256}, 16-B aligned tensors and "
+                  "an input image of at most 32 KiB");
+  hipStream_t s = as_stream(stream);
+  const size_t lds = (size_t)(h * w * c * esz);
+#define RSP(TI, TO)                                                                                          \
+  hipLaunchKernelGGL((resize_pool_nhwc8_img_kernel<TI, TO>), dim3((unsigned)n), dim3(256), lds, s, (const TI*)x, \
+                     (TO*)y, (TO*)pool, (int)c, (int)h, (int)w, (int)oh, (int)ow)
+  if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RSP(float, float);
+  else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) RSP(float, __bf16);
+  else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) RSP(__bf16, __bf16);
+  else RSP(__bf16, float);
+#undef RSP
+  COMET_CHECK_LAUNCH("comet_resize_bilinear_pool_nhwc");
+  return COMET_OK;
+}
+
+extern "C" int comet_conv1x1_resize_pool_nhwc(const void* x, const void* weight, const float* bias, void* y,
+                                              void* pool, int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh,
+                                              int64_t ow, void* stream) {
+  COMET_CHECK_ARG(x && weight && y && pool && n > 0 && h > 0 && w > 0 && oh >= 2 && ow >= 2,
+                  "comet_conv1x1_resize_pool_nhwc: bad args");
+  COMET_CHECK_ARG((c == 32 || c == 64) && (h * w) % 16 == 0 && 2 * h * w * c * 2 <= 65536 && n < (1ll << 31) &&
+                      oh * ow * c < (1ll << 30) &&
+                      ((uintptr_t)x | (uintptr_t)weight | (uintptr_t)y | (uintptr_t)pool) % 16 == 0,
+                  "comet_conv1x1_resize_pool_nhwc: needs c in {32, 64}, h * w % 16 == 0, two input images within "
+                  "64 KiB and 16-B aligned tensors");
+  hipStream_t s = as_stream(stream);
+  const size_t lds = (size_t)(2 * h * w * c * 2);
+  if (c == 32)
+    hipLaunchKernelGGL((conv1x1_resize_pool_kernel<2>), dim3((unsigned)n), dim3(256), lds, s, (const __bf16*)x,
+                       (const __bf16*)weight, bias, (__bf16*)y, (__bf16*)pool, (int)h, (int)w, (int)oh, (int)ow);
+  else
+    hipLaunchKernelGGL((conv1x1_resize_pool_kernel<4>), dim3((unsigned)n), dim3(256), lds, s, (const __bf16*)x,
+                       (const __bf16*)weight, bias, (__bf16*)y, (__bf16*)pool, (int)h, (int)w, (int)oh, (int)ow);
+  COMET_CHECK_LAUNCH("comet_conv1x1_resize_pool_nhwc");
   return COMET_OK;
 }
 

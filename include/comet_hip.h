@@ -292,6 +292,20 @@ int comet_instnorm_nhwc(int dtype, const void* x, const void* res, void* y, int6
 int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, const void* x, void* y,
                           int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
                           int add, void* stream);
+/* NHWC resize (align_corners=True) and the 2 x 2 / stride-2 average pool of its output in one pass
+ * (refine_track.py fine features + blocks.py:371 F.avg_pool2d): y [n, oh, ow, c], pool
+ * [n, oh / 2, ow / 2, c], both equal to comet_resize_bilinear followed by comet_avgpool2_nhwc.
+ * c in {8, 16, 32, 64, 128, 256}, 16-B aligned, input image h * w * c elements of at most 32 KiB. */
+int comet_resize_bilinear_pool_nhwc(int dtype_in, int dtype_out, const void* x, void* y, void* pool,
+                                    int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
+                                    void* stream);
+/* The fine ShallowEncoder's tail (blocks.py:105-110 + the fine pyramid's pool, refine_track.py):
+ * t = x + conv1x1(x; weight [c, c] bf16, bias f32) rounded to bf16 as comet_gemm's narrow kernel
+ * does, then y = resize(t) [n, oh, ow, c] and pool = avgpool2(y), without writing t. bf16 x, y, pool;
+ * c in {32, 64}, h * w % 16 == 0, 2 * h * w * c * 2 <= 64 KiB, 16-B aligned. */
+int comet_conv1x1_resize_pool_nhwc(const void* x, const void* weight, const float* bias, void* y, void* pool,
+                                   int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
+                                   void* stream);
 /* NHWC resize into a channel slice of a wider NHWC tensor (output pixel pitch ldy elements):
  * BasicEncoder's four up-sampled maps land directly in their torch.cat(dim=1) positions
  * (blocks.py:97-107), so the 416-channel concat is never copied. c, ldy % 8 == 0. */

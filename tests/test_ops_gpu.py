@@ -1150,6 +1150,52 @@ def test_gemm_tile_order(mnk, odt, monkeypatch):
     assert bad == 0, f"{mnk} {odt}: max err {err.max().item():.3e}, {bad} bad"
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("geo", [(512, 16, 16, 32, 31, 31), (64, 16, 16, 32, 30, 30), (33, 9, 13, 16, 17, 24),
+                                 (8, 4, 4, 64, 3, 2)])
+def test_resize_bilinear_pool_fused(dtype, geo):
+    """comet_resize_bilinear_pool_nhwc (the fine ShallowEncoder's last up-sampling with the fine
+    pyramid's 2 x 2 average pool, blocks.py:371 / refine_track.py) equals comet_resize_bilinear
+    followed by comet_avgpool2_nhwc bit for bit, odd and even output sizes; and both match torch's
+    F.interpolate(align_corners=True) + F.avg_pool2d."""
+    ops = _ops()
+    n, h, w, c, oh, ow = geo
+    g = torch.Generator(device=DEV).manual_seed(n + oh)
+    x = torch.randn(n, h, w, c, device=DEV, generator=g).to(dtype)
+    y, p = ops.resize_bilinear_pool(x, oh, ow)
+    y_ref = ops.resize_bilinear(x, oh, ow, nhwc=True)
+    p_ref = ops.avgpool2_nhwc(y_ref)
+    assert torch.equal(y, y_ref) and torch.equal(p, p_ref)
+    yt = torch.nn.functional.interpolate(x.permute(0, 3, 1, 2).float(), size=(oh, ow), mode="bilinear",
+                                         align_corners=True)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert (y.permute(0, 3, 1, 2).float() - yt).abs().max().item() <= tol * (1 + yt.abs().max().item())
+    pt = torch.nn.functional.avg_pool2d(y.permute(0, 3, 1, 2).float(), 2, stride=2)
+    assert (p.permute(0, 3, 1, 2).float() - pt).abs().max().item() <= tol * (1 + pt.abs().max().item())
+
+
+@pytest.mark.parametrize("c,n,hw,o", [(32, 128, 16, 31), (32, 64, 16, 30), (64, 256, 8, 15)])
+def test_conv1x1_resize_pool_fused(c, n, hw, o):
+    """comet_conv1x1_resize_pool_nhwc (the fine ShallowEncoder's conv2 + residual, final up-sampling
+    and the fine pyramid's pool, blocks.py:105-110) equals the narrow GEMM (linear with resid = x)
+    followed by resize_bilinear + avgpool2_nhwc bit for bit (M >= 16384 rows: the skinny kernel the
+    unfused path takes), and t = x + conv(x) matches an f64 reference."""
+    ops = _ops()
+    g = torch.Generator(device=DEV).manual_seed(c + n + o)
+    x = torch.randn(n, hw, hw, c, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(c, c, device=DEV, generator=g) * c ** -0.5).to(torch.bfloat16)
+    b = torch.randn(c, device=DEV, generator=g)
+    y, p = ops.conv1x1_resize_pool(x, w, b, o, o)
+    t = ops.linear(x.reshape(-1, c), w, bias=b, resid=x.reshape(-1, c), out_dtype=torch.bfloat16)
+    assert tuple(ops._PLAN)[0] == 0, f"expected the skinny GEMM plan, got {tuple(ops._PLAN)}"
+    tref = (x.reshape(-1, c).double() @ w.double().t() + b.double() + x.reshape(-1, c).double())
+    assert ((t.double() - tref).abs() <= 1e-2 * tref.abs() + 1e-2).all()
+    y_ref = ops.resize_bilinear(t.reshape(n, hw, hw, c), o, o, nhwc=True)
+    p_ref = ops.avgpool2_nhwc(y_ref)
+    assert torch.equal(y, y_ref), f"y: max diff {(y.float() - y_ref.float()).abs().max().item():.3e}"
+    assert torch.equal(p, p_ref), f"pool: max diff {(p.float() - p_ref.float()).abs().max().item():.3e}"
+
+
 def test_cast_multi_and_weight_cache_refresh():
     """comet_cast_multi_f32_bf16 equals torch's RNE .to(bfloat16) bit for bit (aligned and
     unaligned views, > 48 tensors); refresh_weight_cache re-casts cached copies in place after
