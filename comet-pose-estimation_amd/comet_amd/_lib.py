@@ -130,7 +130,8 @@ SIGNATURES = {
     "comet_instnorm_nhwc": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, _F, _INT, _INT, c_vp, c_i64, c_vp]),
     "comet_resize_bilinear": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, _INT, c_vp]),
     "comet_resize_bilinear_pool_nhwc": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
-    "comet_conv1x1_resize_pool_nhwc": (_INT, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    "comet_conv1x1_resize_pool_nhwc": (_INT, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                               c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
     "comet_resize_bilinear_nhwc_into": (_INT, [_INT, _INT, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
                                                _INT, c_vp]),
     "comet_act_fwd": (_INT, [_INT, _INT, _INT, c_vp, c_vp, c_i64, c_vp]),

@@ -23,11 +23,12 @@ def refine_track(images, fine_fnet, fine_tracker, coarse_pred, pradius=15, sradi
     cdt = F.compute_dtype()
     patches, topleft, query = ops.patch_gather(images, coarse_pred, pradius, cdt,
                                                cpad=8 if cdt == torch.bfloat16 else 3)
-    feat, feat1 = fine_fnet(patches, with_pool=True)  # [B*N*S, P, P, 32], its 2x2 average pool
+    # [B*N*S, P, P, 32] and the fine correlation pyramid's levels 1 and 2 (2x2 average pools)
+    feat, feat1, feat2 = fine_fnet(patches, with_pool=2)
     P, C = feat.shape[1], feat.shape[-1]
     feat = feat.reshape(B * N, S, P, P, C)
     preds, _, _, qfeat, _ = fine_tracker(query.reshape(B * N, 1, 2), fmaps=feat, iters=fine_iters, return_feat=True,
-                                         pyramid1=feat1)
+                                         pyramid1=feat1, pyramid2=feat2)
     fine_last = preds[-1].reshape(B * N, S, 2)
     refined = ops.refine_combine(fine_last, topleft, coarse_pred, B, S, N)
     score = inv = None

@@ -61,7 +61,7 @@ class BaseTrackerPredictor(nn.Module):
 
     @torch.no_grad()
     def forward(self, query_points, fmaps=None, iters=4, return_feat=False, down_ratio=1, is_train=False,
-                track_feats=None, TRACKorPOSE=False, ind=0, pyramid1=None):
+                track_feats=None, TRACKorPOSE=False, ind=0, pyramid1=None, pyramid2=None):
         """query_points [B, N, 2]; fmaps NHWC [B, S, HH, WW, C] (compute dtype).
         Returns (coord_preds list of [B, S, N, 2], vis [B, S, N] or None, track_feats [B, N, S, C],
         query_track_feat [B, N, C], conf None)."""
@@ -77,8 +77,10 @@ class BaseTrackerPredictor(nn.Module):
         query_feat = ops.sample_bilinear(fm0, q, border=True)  # [B, N, C]
         track_feats = query_feat.reshape(B, N, 1, C).repeat(1, 1, S, 1).contiguous()  # f32 [B, N, S, C]
         pyr = [fmaps.reshape(B * S, HH, WW, C)]
-        if pyramid1 is not None and self.corr_levels > 1:  # level 1 already pooled by the producer
+        if pyramid1 is not None and self.corr_levels > 1:  # levels 1 (and 2) already pooled by the producer
             pyr.append(pyramid1)
+            if pyramid2 is not None and self.corr_levels > 2:
+                pyr.append(pyramid2)
         while len(pyr) < self.corr_levels:
             pyr.append(ops.avgpool2_nhwc(pyr[-1]))
         pos = ops.sample_bilinear(self._pos_table(HH, WW, dev).expand(B, -1, -1, -1), q, border=True)  # [B, N, tdim]

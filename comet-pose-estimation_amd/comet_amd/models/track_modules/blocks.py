@@ -89,27 +89,31 @@ class ShallowEncoder(nn.Module):
     @torch.no_grad()
     def forward(self, x, with_pool=False):
         """x NHWC [n, P, P, 3] -> NHWC [n, P/stride, P/stride, 32] (with_pool: also its 2x2 average
-        pool, the fine correlation pyramid's level 1: conv2, the residual, the up-sampling and the
-        pool in one kernel, comet_conv1x1_resize_pool_nhwc)."""
+        pool, the fine correlation pyramid's level 1, and with with_pool=2 that pool's pool, level 2:
+        the resize-and-adds, conv2, the residual, the up-sampling and the pools in one kernel,
+        comet_conv1x1_resize_pool_nhwc)."""
         _, H, W, _ = x.shape
         x = ops.instnorm_nhwc(conv2d_nhwc(x, self.conv1, 2, 1), relu=True)
         h, w = x.shape[1], x.shape[2]
-        tmp = self.layer1(x)
-        x = ops.resize_bilinear(tmp, h, w, nhwc=True, out=x, add=True)
-        tmp = self.layer2(tmp)
-        x = ops.resize_bilinear(tmp, h, w, nhwc=True, out=x, add=True)
         n, _, _, c = x.shape
         oh, ow = H // self.stride, W // self.stride
         w2 = F.wcast(self.conv2.weight.reshape(c, c))
-        if with_pool and ops.conv1x1_resize_pool_ok(x, w2, self.conv2.bias):
-            # conv2 (1x1) + residual, up-sampling and the pyramid's pool in one kernel (t never in HBM)
-            return ops.conv1x1_resize_pool(x, w2, self.conv2.bias, oh, ow)
+        tmp1 = self.layer1(x)
+        tmp2 = self.layer2(tmp1)  # (layer2 reads layer1's output, not x: the two adds below can wait)
+        if with_pool and ops.conv1x1_resize_pool_ok(x, w2, self.conv2.bias, tmp1, tmp2):
+            # both resize-and-adds, conv2 (1x1) + residual, the up-sampling and the pyramid's pools
+            # in one kernel (the sums and the conv2 output never in HBM)
+            return ops.conv1x1_resize_pool(x, w2, self.conv2.bias, oh, ow, up1=tmp1, up2=tmp2, pool2=with_pool == 2)
+        x = ops.resize_bilinear(tmp1, h, w, nhwc=True, out=x, add=True)
+        x = ops.resize_bilinear(tmp2, h, w, nhwc=True, out=x, add=True)
         x = F.linear(x.reshape(-1, c), w2, self.conv2.bias, resid=x.reshape(-1, c), out_dtype=x.dtype).reshape(n, h, w, c)
         if with_pool:
             if ops.resize_pool_ok(x):
-                return ops.resize_bilinear_pool(x, oh, ow)
-            y = ops.resize_bilinear(x, oh, ow, nhwc=True)
-            return y, ops.avgpool2_nhwc(y)
+                y, p = ops.resize_bilinear_pool(x, oh, ow)
+            else:
+                y = ops.resize_bilinear(x, oh, ow, nhwc=True)
+                p = ops.avgpool2_nhwc(y)
+            return (y, p, ops.avgpool2_nhwc(p)) if with_pool == 2 else (y, p)
         return ops.resize_bilinear(x, oh, ow, nhwc=True)
 
 

@@ -601,24 +601,33 @@ def resize_bilinear_pool(x, oh, ow):
     return y, p
 
 
-def conv1x1_resize_pool(x, w, b, oh, ow):
-    """NHWC bf16 x [n, h, w, c]: t = x + x W^T + b (W [c, c] bf16, b f32), y = resize(t) to
-    [n, oh, ow, c], pool = avgpool2(y), in one kernel: linear(resid=x) + resize_bilinear_pool bit for
-    bit, without t in HBM (the fine ShallowEncoder's conv2 + up-sampling, blocks.py:105-110)."""
+def conv1x1_resize_pool(x, w, b, oh, ow, up1=None, up2=None, pool2=False):
+    """NHWC bf16 x [n, h, w, c]: x2 = (x + up(up1)) + up(up2) (optional, each rounded to bf16 as
+    resize_bilinear(..., out=x, add=True)), t = x2 + x2 W^T + b (W [c, c] bf16, b f32), y = resize(t)
+    to [n, oh, ow, c], pool = avgpool2(y) (and with pool2: avgpool2(pool)), in one kernel -- the
+    unfused calls bit for bit, without x2 or t in HBM (the fine ShallowEncoder's tail, blocks.py:97-110,
+    and the fine correlation pyramid's levels 1-2)."""
     n, h, ww, c = x.shape
     y = torch.empty(n, oh, ow, c, device=x.device, dtype=x.dtype)
     p = torch.empty(n, oh // 2, ow // 2, c, device=x.device, dtype=x.dtype)
-    L.check(L.load().comet_conv1x1_resize_pool_nhwc(_p(x), _p(w), _p(b), _p(y), _p(p), n, c, h, ww, oh, ow,
-                                                    stream()), "conv1x1_resize_pool")
-    return y, p
+    q = torch.empty(n, oh // 4, ow // 4, c, device=x.device, dtype=x.dtype) if pool2 else None
+    h1, w1 = (up1.shape[1], up1.shape[2]) if up1 is not None else (0, 0)
+    h2, w2 = (up2.shape[1], up2.shape[2]) if up2 is not None else (0, 0)
+    L.check(L.load().comet_conv1x1_resize_pool_nhwc(_p(x), _p(up1), h1, w1, _p(up2), h2, w2, _p(w), _p(b), _p(y),
+                                                    _p(p), _p(q), n, c, h, ww, oh, ow, stream()), "conv1x1_resize_pool")
+    return (y, p, q) if pool2 else (y, p)
 
 
-def conv1x1_resize_pool_ok(x, w, b):
+def conv1x1_resize_pool_ok(x, w, b, *ups):
     n, h, ww, c = x.shape
-    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and c in (32, 64) and x.is_contiguous()
-            and w.is_contiguous() and tuple(w.shape) == (c, c) and (h * ww) % 16 == 0 and 4 * h * ww * c <= 65536
-            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
-            and (b is None or (b.dtype == torch.float32 and b.is_contiguous())))
+    ok = (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and c in (32, 64) and x.is_contiguous()
+          and w.is_contiguous() and tuple(w.shape) == (c, c) and (h * ww) % 16 == 0 and 4 * h * ww * c <= 49152
+          and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+          and (b is None or (b.dtype == torch.float32 and b.is_contiguous())))
+    for u in ups:
+        ok = ok and (u.dtype == torch.bfloat16 and u.is_contiguous() and u.shape[0] == n and u.shape[3] == c
+                     and u.data_ptr() % 16 == 0)
+    return ok
 
 
 def resize_pool_ok(x):

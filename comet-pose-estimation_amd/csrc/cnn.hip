@@ -200,9 +200,10 @@ resize_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, int c, int
 // are padded to an even column count so a column pair never straddles a wave (64 % (2 * c / 8) == 0:
 // c in {8, 16, 32, 64, 128, 256}); the odd last row of y (floor pooling drops it) is written after.
 // (workgroup body) y / pool of image ni from the staged input image `img` in LDS
+// (and, when pl != nullptr, a copy of the image's pool in LDS, [oh / 2][ow / 2][c], for a second level)
 template <typename TI, typename TO>
 __device__ __forceinline__ void resize_pool_body(const TI* img, TO* __restrict__ y, TO* __restrict__ pool, int64_t ni,
-                                                 int c, int h, int w, int oh, int ow) {
+                                                 int c, int h, int w, int oh, int ow, TO* pl = nullptr) {
   const int cg8 = c / 8, ph = oh / 2, pw = ow / 2;
   const int rpi = ((ow + 1) / 2) * 2 * cg8;  // lanes per row pair (even column count)
   const int lane = threadIdx.x & 63;
@@ -247,7 +248,10 @@ __device__ __forceinline__ void resize_pool_body(const TI* img, TO* __restrict__
       const float b = __shfl_down(a[e], cg8, 64), d = __shfl_down(cq[e], cg8, 64);
       o[e] = (a[e] + b + cq[e] + d) * 0.25f;
     }
-    if (live && (ox & 1) == 0 && ox / 2 < pw) store8(po + ((int64_t)py * pw + ox / 2) * c + cg * 8, o);
+    if (live && (ox & 1) == 0 && ox / 2 < pw) {
+      store8(po + ((int64_t)py * pw + ox / 2) * c + cg * 8, o);
+      if (pl != nullptr) store8(pl + (py * pw + ox / 2) * c + cg * 8, o);
+    }
   }
   if (oh & 1) {  // the last row of y (no pool)
     for (int it = threadIdx.x; it < ow * cg8; it += 256) {
@@ -272,27 +276,52 @@ resize_pool_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, TO* _
   resize_pool_body<TI, TO>(reinterpret_cast<const TI*>(img_lds), y, pool, ni, c, h, w, oh, ow);
 }
 
-// The fine ShallowEncoder's tail in one pass per patch (blocks.py:105-110 with refine_track's pool):
-// t = x + conv2(x) (1x1, C x C, bias; the skinny GEMM's MFMA and epilogue, bit for bit: same
-// instruction on the same operands; its epilogue at alpha = beta = 1 is two exact-product fmas, i.e. the
-// adds (acc + bias) + x, rounded to bf16), then
-// y = resize(t) and pool = avgpool2(y) as resize_pool_nhwc8_img_kernel. x, t stay in LDS: the [n, h, w,
-// C] conv2 output never reaches HBM (one 16.7M-row GEMM and its 3.2 GB of traffic per step less).
-// bf16, C = 32 x NT16 / 2 (NT16 16-column MFMA tiles, one 32-deep k step per 32 input channels).
+// The fine ShallowEncoder's tail in one pass per patch (blocks.py:97-110 with refine_track's pool):
+//   x1 = x + up(u1) (rounded), x2 = x1 + up(u2) (rounded)  -- the two resize-and-add steps, optional
+//   t = x2 + conv2(x2) (1x1, C x C, bias: the skinny GEMM's MFMA on the same operands; its epilogue at
+//       alpha = beta = 1 is two exact-product fmas, i.e. the adds (acc + bias) + x2, rounded to bf16)
+//   y = resize(t), pool = avgpool2(y)  (as resize_pool_nhwc8_img_kernel), pool2 = avgpool2(pool) (optional:
+//       the fine correlation pyramid's level 2, base_track_predictor.py:83 / blocks.py:371)
+// x2 and t stay in LDS: neither the [n, h, w, C] sums nor the conv2 output reach HBM (two resize-add
+// passes and one 16.7M-row GEMM per step fewer). bf16, C = 16 x NT16 (one 32-deep k step per 32
+// input channels).
 template <int NT16>
 __global__ void __launch_bounds__(256)
-conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ wt, const float* __restrict__ bias,
-                           __bf16* __restrict__ y, __bf16* __restrict__ pool, int h, int w, int oh, int ow) {
-  constexpr int C = NT16 * 16, KC = C / 32;
+conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ u1, int h1, int w1,
+                           const __bf16* __restrict__ u2, int h2, int w2, const __bf16* __restrict__ wt,
+                           const float* __restrict__ bias, __bf16* __restrict__ y, __bf16* __restrict__ pool,
+                           __bf16* __restrict__ pool2, int h, int w, int oh, int ow) {
+  constexpr int C = NT16 * 16, KC = C / 32, CG8 = C / 8;
   extern __shared__ uint4 img_lds[];
   const int64_t ni = blockIdx.x;
   const int hw = h * w;
   const int nvec = hw * C * 2 / 16;
   const uint4* src = reinterpret_cast<const uint4*>(x + ni * hw * C);
   for (int i = threadIdx.x; i < nvec; i += 256) img_lds[i] = src[i];
-  const __bf16* xs = reinterpret_cast<const __bf16*>(img_lds);
+  __bf16* xs = reinterpret_cast<__bf16*>(img_lds);
   __bf16* ts = reinterpret_cast<__bf16*>(img_lds + nvec);
   const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  // x += up(u), rounded, in place in LDS (each thread owns the same 8-channel groups it adds to)
+  auto upadd = [&](const __bf16* __restrict__ u, int hu, int wu) {
+    const __bf16* ub = u + ni * hu * wu * C;
+    for (int it = threadIdx.x; it < hw * CG8; it += 256) {
+      const int pix = it / CG8, cg = it - pix * CG8;
+      const int oy = pix / w, ox = pix - oy * w;
+      int64_t y0, y1, x0, x1;
+      float fy, fx;
+      ac_coord(oy, hu, h, y0, y1, fy);
+      ac_coord(ox, wu, w, x0, x1, fx);
+      float v00[8], v01[8], v10[8], v11[8], o[8];
+      load8(ub + ((int)y0 * wu + (int)x0) * C + cg * 8, v00);
+      load8(ub + ((int)y0 * wu + (int)x1) * C + cg * 8, v01);
+      load8(ub + ((int)y1 * wu + (int)x0) * C + cg * 8, v10);
+      load8(ub + ((int)y1 * wu + (int)x1) * C + cg * 8, v11);
+      load8(xs + pix * C + cg * 8, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = o[e] + bilerp(v00[e], v01[e], v10[e], v11[e], fx, fy);
+      store8(xs + pix * C + cg * 8, o);
+    }
+  };
   bf16x8 bf[NT16][KC];
 #pragma unroll
   for (int nt = 0; nt < NT16; ++nt)
@@ -304,6 +333,14 @@ conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) b4[nt][r] = bias != nullptr ? bias[nt * 16 + 4 * g + r] : 0.f;
   __syncthreads();
+  if (u1 != nullptr) {
+    upadd(u1, h1, w1);
+    __syncthreads();
+  }
+  if (u2 != nullptr) {
+    upadd(u2, h2, w2);
+    __syncthreads();
+  }
   for (int m0 = wv * 16; m0 < hw; m0 += 64) {  // 16 pixels per wave step (hw % 16 == 0, host-checked)
     const int m = m0 + li;
     f32x4 acc[NT16];
@@ -328,7 +365,26 @@ conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restric
     }
   }
   __syncthreads();
-  resize_pool_body<__bf16, __bf16>(ts, y, pool, ni, C, h, w, oh, ow);
+  __bf16* pl = pool2 != nullptr ? ts + hw * C : nullptr;
+  resize_pool_body<__bf16, __bf16>(ts, y, pool, ni, C, h, w, oh, ow, pl);
+  if (pool2 == nullptr) return;
+  // the second pyramid level: avgpool2 of the pool, from its LDS copy (avgpool2_rows_kernel's order)
+  __syncthreads();
+  const int ph = oh / 2, pw = ow / 2, qh = ph / 2, qw = pw / 2;
+  __bf16* qo = pool2 + ni * qh * qw * C;
+  for (int it = threadIdx.x; it < qh * qw * CG8; it += 256) {
+    const int q = it / CG8, cg = it - q * CG8, qy = q / qw, qx = q - qy * qw;
+    const __bf16* r0 = pl + ((2 * qy) * pw + 2 * qx) * C + cg * 8;
+    const __bf16* r1 = r0 + pw * C;
+    float a[8], bq[8], cq[8], d[8], o[8];
+    load8(r0, a);
+    load8(r0 + C, bq);
+    load8(r1, cq);
+    load8(r1 + C, d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (a[e] + bq[e] + cq[e] + d[e]) * 0.25f;
+    store8(qo + (int64_t)q * C + cg * 8, o);
+  }
 }
 
 inline unsigned g1d(int64_t n) {
@@ -436,24 +492,31 @@ extern "C" int comet_resize_bilinear_pool_nhwc(int dtype_in, int dtype_out, cons
   return COMET_OK;
 }
 
-extern "C" int comet_conv1x1_resize_pool_nhwc(const void* x, const void* weight, const float* bias, void* y,
-                                              void* pool, int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh,
-                                              int64_t ow, void* stream) {
+extern "C" int comet_conv1x1_resize_pool_nhwc(const void* x, const void* up1, int64_t h1, int64_t w1, const void* up2,
+                                              int64_t h2, int64_t w2, const void* weight, const float* bias, void* y,
+                                              void* pool, void* pool2, int64_t n, int64_t c, int64_t h, int64_t w,
+                                              int64_t oh, int64_t ow, void* stream) {
   COMET_CHECK_ARG(x && weight && y && pool && n > 0 && h > 0 && w > 0 && oh >= 2 && ow >= 2,
                   "comet_conv1x1_resize_pool_nhwc: bad args");
-  COMET_CHECK_ARG((c == 32 || c == 64) && (h * w) % 16 == 0 && 2 * h * w * c * 2 <= 65536 && n < (1ll << 31) &&
-                      oh * ow * c < (1ll << 30) &&
-                      ((uintptr_t)x | (uintptr_t)weight | (uintptr_t)y | (uintptr_t)pool) % 16 == 0,
+  const int64_t lds_b = 2 * h * w * c * 2 + (pool2 != nullptr ? (oh / 2) * (ow / 2) * c * 2 : 0);
+  COMET_CHECK_ARG((c == 32 || c == 64) && (h * w) % 16 == 0 && lds_b <= 65536 && n < (1ll << 31) &&
+                      oh * ow * c < (1ll << 30) && (pool2 == nullptr || (oh >= 4 && ow >= 4)) &&
+                      ((uintptr_t)x | (uintptr_t)up1 | (uintptr_t)up2 | (uintptr_t)weight | (uintptr_t)y |
+                       (uintptr_t)pool | (uintptr_t)pool2) % 16 == 0,
                   "comet_conv1x1_resize_pool_nhwc: needs c in {32, 64}, h * w % 16 == 0, two input images within "
                   "64 KiB and 16-B aligned tensors");
+  COMET_CHECK_ARG((up1 == nullptr || (h1 > 0 && w1 > 0)) && (up2 == nullptr || (h2 > 0 && w2 > 0)),
+                  "comet_conv1x1_resize_pool_nhwc: bad up-sampled input size");
   hipStream_t s = as_stream(stream);
-  const size_t lds = (size_t)(2 * h * w * c * 2);
-  if (c == 32)
-    hipLaunchKernelGGL((conv1x1_resize_pool_kernel<2>), dim3((unsigned)n), dim3(256), lds, s, (const __bf16*)x,
-                       (const __bf16*)weight, bias, (__bf16*)y, (__bf16*)pool, (int)h, (int)w, (int)oh, (int)ow);
-  else
-    hipLaunchKernelGGL((conv1x1_resize_pool_kernel<4>), dim3((unsigned)n), dim3(256), lds, s, (const __bf16*)x,
-                       (const __bf16*)weight, bias, (__bf16*)y, (__bf16*)pool, (int)h, (int)w, (int)oh, (int)ow);
+  const size_t lds = (size_t)lds_b;
+#define C1P(NT)                                                                                                   \
+  hipLaunchKernelGGL((conv1x1_resize_pool_kernel<NT>), dim3((unsigned)n), dim3(256), lds, s, (const __bf16*)x,      \
+                     (const __bf16*)up1, (int)h1, (int)w1, (const __bf16*)up2, (int)h2, (int)w2,                     \
+                     (const __bf16*)weight, bias, (__bf16*)y, (__bf16*)pool, (__bf16*)pool2, (int)h, (int)w, (int)oh, \
+                     (int)ow)
+  if (c == 32) C1P(2);
+  else C1P(4);
+#undef C1P
   COMET_CHECK_LAUNCH("comet_conv1x1_resize_pool_nhwc");
   return COMET_OK;
 }

@@ -299,13 +299,17 @@ int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, const void* x, 
 int comet_resize_bilinear_pool_nhwc(int dtype_in, int dtype_out, const void* x, void* y, void* pool,
                                     int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
                                     void* stream);
-/* The fine ShallowEncoder's tail (blocks.py:105-110 + the fine pyramid's pool, refine_track.py):
- * t = x + conv1x1(x; weight [c, c] bf16, bias f32) rounded to bf16 as comet_gemm's narrow kernel
- * does, then y = resize(t) [n, oh, ow, c] and pool = avgpool2(y), without writing t. bf16 x, y, pool;
- * c in {32, 64}, h * w % 16 == 0, 2 * h * w * c * 2 <= 64 KiB, 16-B aligned. */
-int comet_conv1x1_resize_pool_nhwc(const void* x, const void* weight, const float* bias, void* y, void* pool,
-                                   int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
-                                   void* stream);
+/* The fine ShallowEncoder's tail (blocks.py:97-110 + the fine pyramid's pool, refine_track.py):
+ * x2 = (x + up(up1)) + up(up2) (each sum rounded to bf16, as two resize-and-add calls; up1 / up2
+ * optional, [n, h1, w1, c] / [n, h2, w2, c], align_corners=True), t = x2 + conv1x1(x2; weight
+ * [c, c] bf16, bias f32) rounded as comet_gemm's narrow kernel does, y = resize(t) [n, oh, ow, c] and
+ * pool = avgpool2(y), and optionally pool2 = avgpool2(pool) [n, oh / 4, ow / 4, c] (the pyramid's
+ * next level), without writing x2 or t. bf16 tensors; c in {32, 64}, h * w % 16 == 0,
+ * 2 * h * w * c * 2 (+ (oh / 2) * (ow / 2) * c * 2 with pool2) <= 64 KiB, 16-B aligned. */
+int comet_conv1x1_resize_pool_nhwc(const void* x, const void* up1, int64_t h1, int64_t w1, const void* up2,
+                                   int64_t h2, int64_t w2, const void* weight, const float* bias, void* y,
+                                   void* pool, void* pool2, int64_t n, int64_t c, int64_t h, int64_t w,
+                                   int64_t oh, int64_t ow, void* stream);
 /* NHWC resize into a channel slice of a wider NHWC tensor (output pixel pitch ldy elements):
  * BasicEncoder's four up-sampled maps land directly in their torch.cat(dim=1) positions
  * (blocks.py:97-107), so the 416-channel concat is never copied. c, ldy % 8 == 0. */

@@ -1174,26 +1174,37 @@ def test_resize_bilinear_pool_fused(dtype, geo):
     assert (p.permute(0, 3, 1, 2).float() - pt).abs().max().item() <= tol * (1 + pt.abs().max().item())
 
 
+@pytest.mark.parametrize("ups", [0, 2])
 @pytest.mark.parametrize("c,n,hw,o", [(32, 128, 16, 31), (32, 64, 16, 30), (64, 256, 8, 15)])
-def test_conv1x1_resize_pool_fused(c, n, hw, o):
-    """comet_conv1x1_resize_pool_nhwc (the fine ShallowEncoder's conv2 + residual, final up-sampling
-    and the fine pyramid's pool, blocks.py:105-110) equals the narrow GEMM (linear with resid = x)
-    followed by resize_bilinear + avgpool2_nhwc bit for bit (M >= 16384 rows: the skinny kernel the
-    unfused path takes), and t = x + conv(x) matches an f64 reference."""
+def test_conv1x1_resize_pool_fused(c, n, hw, o, ups):
+    """comet_conv1x1_resize_pool_nhwc (the fine ShallowEncoder's tail, blocks.py:97-110: the two
+    resize-and-adds of layer1 / layer2's outputs, conv2 + residual, the final up-sampling and the
+    fine pyramid's levels 1 and 2) equals the unfused calls bit for bit -- resize_bilinear(out=x, add=True)
+    twice, the narrow GEMM (linear with resid, M >= 16384 rows: the skinny kernel), resize_bilinear
+    and avgpool2_nhwc -- and t matches an f64 reference."""
     ops = _ops()
-    g = torch.Generator(device=DEV).manual_seed(c + n + o)
+    g = torch.Generator(device=DEV).manual_seed(c + n + o + ups)
     x = torch.randn(n, hw, hw, c, device=DEV, generator=g).to(torch.bfloat16)
+    u1 = torch.randn(n, hw // 2, hw // 2, c, device=DEV, generator=g).to(torch.bfloat16) if ups else None
+    u2 = torch.randn(n, hw // 4, hw // 4, c, device=DEV, generator=g).to(torch.bfloat16) if ups else None
     w = (torch.randn(c, c, device=DEV, generator=g) * c ** -0.5).to(torch.bfloat16)
     b = torch.randn(c, device=DEV, generator=g)
-    y, p = ops.conv1x1_resize_pool(x, w, b, o, o)
-    t = ops.linear(x.reshape(-1, c), w, bias=b, resid=x.reshape(-1, c), out_dtype=torch.bfloat16)
+    y, p, q = ops.conv1x1_resize_pool(x, w, b, o, o, up1=u1, up2=u2, pool2=True)
+    y2, p2 = ops.conv1x1_resize_pool(x, w, b, o, o, up1=u1, up2=u2)
+    assert torch.equal(y, y2) and torch.equal(p, p2)
+    x2 = x.clone()
+    if ups:
+        ops.resize_bilinear(u1, hw, hw, nhwc=True, out=x2, add=True)
+        ops.resize_bilinear(u2, hw, hw, nhwc=True, out=x2, add=True)
+    t = ops.linear(x2.reshape(-1, c), w, bias=b, resid=x2.reshape(-1, c), out_dtype=torch.bfloat16)
     assert tuple(ops._PLAN)[0] == 0, f"expected the skinny GEMM plan, got {tuple(ops._PLAN)}"
-    tref = (x.reshape(-1, c).double() @ w.double().t() + b.double() + x.reshape(-1, c).double())
+    tref = (x2.reshape(-1, c).double() @ w.double().t() + b.double() + x2.reshape(-1, c).double())
     assert ((t.double() - tref).abs() <= 1e-2 * tref.abs() + 1e-2).all()
     y_ref = ops.resize_bilinear(t.reshape(n, hw, hw, c), o, o, nhwc=True)
     p_ref = ops.avgpool2_nhwc(y_ref)
     assert torch.equal(y, y_ref), f"y: max diff {(y.float() - y_ref.float()).abs().max().item():.3e}"
     assert torch.equal(p, p_ref), f"pool: max diff {(p.float() - p_ref.float()).abs().max().item():.3e}"
+    assert torch.equal(q, ops.avgpool2_nhwc(p_ref)), "second pyramid level differs"
 
 
 def test_cast_multi_and_weight_cache_refresh():

@@ -17,17 +17,27 @@ from tile_bench import timed  # noqa: E402
 
 def main():
     x = torch.randn(65536, 16, 16, 32, device="cuda").to(torch.bfloat16)
+    u1 = torch.randn(65536, 8, 8, 32, device="cuda").to(torch.bfloat16)
+    u2 = torch.randn(65536, 4, 4, 32, device="cuda").to(torch.bfloat16)
     w = (torch.randn(32, 32, device="cuda") * 0.2).to(torch.bfloat16)
     b = torch.randn(32, device="cuda")
-    conv = lambda: ops.linear(x.reshape(-1, 32), w, bias=b, resid=x.reshape(-1, 32), out_dtype=torch.bfloat16)  # noqa: E731
+
+    def unfused():  # round 5: two resize-adds, the skinny GEMM, resize, avgpool2
+        x2 = x.clone()
+        ops.resize_bilinear(u1, 16, 16, nhwc=True, out=x2, add=True)
+        ops.resize_bilinear(u2, 16, 16, nhwc=True, out=x2, add=True)
+        t = ops.linear(x2.reshape(-1, 32), w, bias=b, resid=x2.reshape(-1, 32), out_dtype=torch.bfloat16)
+        return ops.avgpool2_nhwc(ops.resize_bilinear(t.reshape(x.shape), 31, 31, nhwc=True))
+
+    clone = lambda: x.clone()  # noqa: E731
     sep = lambda: ops.avgpool2_nhwc(ops.resize_bilinear(x, 31, 31, nhwc=True))  # noqa: E731
     fused = lambda: ops.resize_bilinear_pool(x, 31, 31)  # noqa: E731
-    tail = lambda: ops.conv1x1_resize_pool(x, w, b, 31, 31)  # noqa: E731
-    nbytes = x.numel() * 2 + 65536 * (31 * 31 + 15 * 15) * 32 * 2
+    tail = lambda: ops.conv1x1_resize_pool(x, w, b, 31, 31, up1=u1, up2=u2)  # noqa: E731
+    nbytes = (x.numel() + u1.numel() + u2.numel()) * 2 + 65536 * (31 * 31 + 15 * 15) * 32 * 2
     for rep in range(2):
-        c, a, f, t = timed(conv), timed(sep), timed(fused), timed(tail)
-        print(f"conv2 GEMM {c:7.1f} us + resize, avgpool2 {a:7.1f} us | + resize_pool {f:7.1f} us "
-              f"({nbytes / f / 1e6:.2f} TB/s) | conv1x1_resize_pool {t:7.1f} us ({nbytes / t / 1e6:.2f} TB/s)", flush=True)
+        uf, cl, a, f, t = timed(unfused), timed(clone), timed(sep), timed(fused), timed(tail)
+        print(f"unfused tail {uf - cl:7.1f} us (clone excluded) | resize + avgpool2 {a:7.1f} us | resize_pool {f:7.1f} us "
+              f"| conv1x1_resize_pool with both adds {t:7.1f} us ({nbytes / t / 1e6:.2f} TB/s algorithmic)", flush=True)
 
 
 if __name__ == "__main__":
