@@ -282,9 +282,9 @@ resize_pool_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, TO* _
 //       alpha = beta = 1 is two exact-product fmas, i.e. the adds (acc + bias) + x2, rounded to bf16)
 //   y = resize(t), pool = avgpool2(y)  (as resize_pool_nhwc8_img_kernel), pool2 = avgpool2(pool) (optional:
 //       the fine correlation pyramid's level 2, base_track_predictor.py:83 / blocks.py:371)
-// x2 and t stay in LDS: neither the [n, h, w, C] sums nor the conv2 output reach HBM (two resize-add
-// passes and one 16.7M-row GEMM per step fewer). bf16, C = 16 x NT16 (one 32-deep k step per 32
-// input channels).
+// x2 and t stay in LDS (one image buffer, t written over x2): neither the [n, h, w, C] sums nor the
+// conv2 output reach HBM (two resize-add passes and one 16.7M-row GEMM per step fewer). bf16,
+// C = 16 x NT16 (one 32-deep k step per 32 input channels).
 template <int NT16>
 __global__ void __launch_bounds__(256)
 conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ u1, int h1, int w1,
@@ -292,36 +292,28 @@ conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restric
                            const float* __restrict__ bias, __bf16* __restrict__ y, __bf16* __restrict__ pool,
                            __bf16* __restrict__ pool2, int h, int w, int oh, int ow) {
   constexpr int C = NT16 * 16, KC = C / 32, CG8 = C / 8;
+  // LDS: x (becomes x2, then t in place) | u1 | u2 | the pool's copy (pool2 only)
   extern __shared__ uint4 img_lds[];
   const int64_t ni = blockIdx.x;
   const int hw = h * w;
-  const int nvec = hw * C * 2 / 16;
-  const uint4* src = reinterpret_cast<const uint4*>(x + ni * hw * C);
-  for (int i = threadIdx.x; i < nvec; i += 256) img_lds[i] = src[i];
-  __bf16* xs = reinterpret_cast<__bf16*>(img_lds);
-  __bf16* ts = reinterpret_cast<__bf16*>(img_lds + nvec);
-  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
-  // x += up(u), rounded, in place in LDS (each thread owns the same 8-channel groups it adds to)
-  auto upadd = [&](const __bf16* __restrict__ u, int hu, int wu) {
-    const __bf16* ub = u + ni * hu * wu * C;
-    for (int it = threadIdx.x; it < hw * CG8; it += 256) {
-      const int pix = it / CG8, cg = it - pix * CG8;
-      const int oy = pix / w, ox = pix - oy * w;
-      int64_t y0, y1, x0, x1;
-      float fy, fx;
-      ac_coord(oy, hu, h, y0, y1, fy);
-      ac_coord(ox, wu, w, x0, x1, fx);
-      float v00[8], v01[8], v10[8], v11[8], o[8];
-      load8(ub + ((int)y0 * wu + (int)x0) * C + cg * 8, v00);
-      load8(ub + ((int)y0 * wu + (int)x1) * C + cg * 8, v01);
-      load8(ub + ((int)y1 * wu + (int)x0) * C + cg * 8, v10);
-      load8(ub + ((int)y1 * wu + (int)x1) * C + cg * 8, v11);
-      load8(xs + pix * C + cg * 8, o);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = o[e] + bilerp(v00[e], v01[e], v10[e], v11[e], fx, fy);
-      store8(xs + pix * C + cg * 8, o);
+  const int nvec = hw * C * 2 / 16, n1 = u1 != nullptr ? h1 * w1 * C * 2 / 16 : 0,
+            n2 = u2 != nullptr ? h2 * w2 * C * 2 / 16 : 0;
+  {  // every global load of the workgroup's inputs issued before any wait
+    const uint4* src = reinterpret_cast<const uint4*>(x + ni * hw * C);
+    for (int i = threadIdx.x; i < nvec; i += 256) img_lds[i] = src[i];
+    if (n1) {
+      const uint4* s1 = reinterpret_cast<const uint4*>(u1 + ni * h1 * w1 * C);
+      for (int i = threadIdx.x; i < n1; i += 256) img_lds[nvec + i] = s1[i];
     }
-  };
+    if (n2) {
+      const uint4* s2 = reinterpret_cast<const uint4*>(u2 + ni * h2 * w2 * C);
+      for (int i = threadIdx.x; i < n2; i += 256) img_lds[nvec + n1 + i] = s2[i];
+    }
+  }
+  __bf16* xs = reinterpret_cast<__bf16*>(img_lds);
+  const __bf16* us1 = reinterpret_cast<const __bf16*>(img_lds + nvec);
+  const __bf16* us2 = reinterpret_cast<const __bf16*>(img_lds + nvec + n1);
+  const int lane = threadIdx.x & 63, li = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
   bf16x8 bf[NT16][KC];
 #pragma unroll
   for (int nt = 0; nt < NT16; ++nt)
@@ -333,14 +325,42 @@ conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) b4[nt][r] = bias != nullptr ? bias[nt * 16 + 4 * g + r] : 0.f;
   __syncthreads();
-  if (u1 != nullptr) {
-    upadd(u1, h1, w1);
+  // x2 = round(round(x + up(u1)) + up(u2)), in place (each item owns its 8 channels of one pixel)
+  auto up = [&](const __bf16* ub, int hu, int wu, int oy, int ox, int cg, float (&o)[8]) {
+    int64_t y0, y1, x0, x1;
+    float fy, fx;
+    ac_coord(oy, hu, h, y0, y1, fy);
+    ac_coord(ox, wu, w, x0, x1, fx);
+    float v00[8], v01[8], v10[8], v11[8];
+    load8(ub + ((int)y0 * wu + (int)x0) * C + cg * 8, v00);
+    load8(ub + ((int)y0 * wu + (int)x1) * C + cg * 8, v01);
+    load8(ub + ((int)y1 * wu + (int)x0) * C + cg * 8, v10);
+    load8(ub + ((int)y1 * wu + (int)x1) * C + cg * 8, v11);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = bilerp(v00[e], v01[e], v10[e], v11[e], fx, fy);
+  };
+  if (n1 || n2) {
+    for (int it = threadIdx.x; it < hw * CG8; it += 256) {
+      const int pix = it / CG8, cg = it - pix * CG8;
+      const int oy = pix / w, ox = pix - oy * w;
+      float o[8], v[8];
+      load8(xs + pix * C + cg * 8, o);
+      if (n1) {
+        up(us1, h1, w1, oy, ox, cg, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = to_f32(from_f32<__bf16>(o[e] + v[e]));  // the first add's stored value
+      }
+      if (n2) {
+        up(us2, h2, w2, oy, ox, cg, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = o[e] + v[e];
+      }
+      store8(xs + pix * C + cg * 8, o);
+    }
     __syncthreads();
   }
-  if (u2 != nullptr) {
-    upadd(u2, h2, w2);
-    __syncthreads();
-  }
+  // t = x2 + conv2(x2), written over x2: a wave reads its 16 rows (fragments, residual) before it
+  // writes them (the writes depend on the MFMA that consumed the reads), and no other wave reads them
   for (int m0 = wv * 16; m0 < hw; m0 += 64) {  // 16 pixels per wave step (hw % 16 == 0, host-checked)
     const int m = m0 + li;
     f32x4 acc[NT16];
@@ -352,21 +372,23 @@ conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restric
 #pragma unroll
       for (int nt = 0; nt < NT16; ++nt) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[nt][k], a, acc[nt], 0, 0, 0);
     }
+    float rr[NT16][4];
+#pragma unroll
+    for (int nt = 0; nt < NT16; ++nt) load4(xs + m * C + nt * 16 + 4 * g, rr[nt]);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every read of these rows done before the writes
 #pragma unroll
     for (int nt = 0; nt < NT16; ++nt) {
-      const int n0 = nt * 16 + 4 * g;
-      float rr[4], v[4];
-      load4(xs + m * C + n0, rr);
+      float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = acc[nt][r] + b4[nt][r];  // = fma(alpha = 1, acc, bias) exactly
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = rr[r] + v[r];  // = fma(beta = 1, resid, v) exactly
-      store4(ts + m * C + n0, v);
+      for (int r = 0; r < 4; ++r) v[r] = rr[nt][r] + v[r];  // = fma(beta = 1, resid, v) exactly
+      store4(xs + m * C + nt * 16 + 4 * g, v);
     }
   }
   __syncthreads();
-  __bf16* pl = pool2 != nullptr ? ts + hw * C : nullptr;
-  resize_pool_body<__bf16, __bf16>(ts, y, pool, ni, C, h, w, oh, ow, pl);
+  __bf16* pl = pool2 != nullptr ? reinterpret_cast<__bf16*>(img_lds + nvec + n1 + n2) : nullptr;
+  resize_pool_body<__bf16, __bf16>(xs, y, pool, ni, C, h, w, oh, ow, pl);
   if (pool2 == nullptr) return;
   // the second pyramid level: avgpool2 of the pool, from its LDS copy (avgpool2_rows_kernel's order)
   __syncthreads();
@@ -498,13 +520,14 @@ extern "C" int comet_conv1x1_resize_pool_nhwc(const void* x, const void* up1, in
                                               int64_t oh, int64_t ow, void* stream) {
   COMET_CHECK_ARG(x && weight && y && pool && n > 0 && h > 0 && w > 0 && oh >= 2 && ow >= 2,
                   "comet_conv1x1_resize_pool_nhwc: bad args");
-  const int64_t lds_b = 2 * h * w * c * 2 + (pool2 != nullptr ? (oh / 2) * (ow / 2) * c * 2 : 0);
+  const int64_t lds_b = (h * w + (up1 ? h1 * w1 : 0) + (up2 ? h2 * w2 : 0)) * c * 2 +
+                        (pool2 != nullptr ? (oh / 2) * (ow / 2) * c * 2 : 0);
   COMET_CHECK_ARG((c == 32 || c == 64) && (h * w) % 16 == 0 && lds_b <= 65536 && n < (1ll << 31) &&
                       oh * ow * c < (1ll << 30) && (pool2 == nullptr || (oh >= 4 && ow >= 4)) &&
                       ((uintptr_t)x | (uintptr_t)up1 | (uintptr_t)up2 | (uintptr_t)weight | (uintptr_t)y |
                        (uintptr_t)pool | (uintptr_t)pool2) % 16 == 0,
-                  "comet_conv1x1_resize_pool_nhwc: needs c in {32, 64}, h * w % 16 == 0, two input images within "
-                  "64 KiB and 16-B aligned tensors");
+                  "comet_conv1x1_resize_pool_nhwc: needs c in {32, 64}, h * w % 16 == 0, the inputs (and the pool "
+                  "copy) within 64 KiB of LDS and 16-B aligned tensors");
   COMET_CHECK_ARG((up1 == nullptr || (h1 > 0 && w1 > 0)) && (up2 == nullptr || (h2 > 0 && w2 > 0)),
                   "comet_conv1x1_resize_pool_nhwc: bad up-sampled input size");
   hipStream_t s = as_stream(stream);
