@@ -871,9 +871,11 @@ def test_corr_sample_mfma_matches_valu_headline(monkeypatch):
     a, v = outs[0][ok], outs[1][ok]
     assert torch.isfinite(a).all()
     # both sum 128 exact products in f32, in different orders: the difference is f32 rounding of
-    # sums whose terms reach ~|v|max, so it is bounded against the output scale, not per element
+    # sums whose terms reach ~|v|max, so it is bounded against the output scale, not per element:
+    # at most ~128 roundings of 2^-24 (7.6e-6); observed 1.5-2.3e-6 (the VALU kernel's add order
+    # moved when the library stopped SLP-packing its f32 adds, round 6)
     err = ((a - v).abs().max() / v.abs().max()).item()
-    assert err < 2e-6, err
+    assert err < 8e-6, err
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
