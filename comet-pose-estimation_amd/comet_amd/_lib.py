@@ -163,7 +163,7 @@ SIGNATURES = {
                                      c_i64, c_i64, _INT, c_vp]),
     "comet_corr_sample": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, _INT, _INT, _INT, c_vp, c_vp, c_vp, c_i64, c_i64,
                                  c_i64, c_i64, _INT, c_vp]),
-    "comet_tracker_tokens": (_INT, [_INT, c_vp, c_vp, _INT, c_vp, c_i64, _INT, c_vp, _INT, c_vp, c_i64, _INT, c_vp]),
+    "comet_tracker_tokens": (_INT, [_INT, c_vp, c_vp, _INT, c_vp, c_i64, _INT, c_vp, _INT, c_vp, c_i64, c_i64, _INT, c_vp]),
     "comet_coords_update": (_INT, [_INT, c_vp, c_vp, c_i64, c_vp, _F, c_i64, c_i64, _INT, c_vp]),
     "comet_avgpool2_nhwc": (_INT, [_INT, c_vp, c_vp, c_i64, _INT, _INT, _INT, c_vp]),
     "comet_patch_gather": (_INT, [_INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, _INT, c_i64, _INT, _INT, _INT, _INT, c_vp]),

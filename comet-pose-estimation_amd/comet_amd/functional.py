@@ -808,6 +808,24 @@ def harmonic(x, freqs, append_input, diag_cov=None):
     return ops.harmonic_fwd(x, freqs, append_input, diag_cov)
 
 
+def wcast_kpad(w, kpad):
+    """Linear weight [N, K] in the compute dtype with its K columns zero-padded to kpad (cached like
+    wcast_conv): the operand for inputs whose rows carry zero padding up to a 64-deep k-tile multiple,
+    so the GEMM takes the persistent kernel (K % 64 == 0) with the same products and sums."""
+    dt = compute_dtype()
+    n, k = w.shape
+    key = ("conv", w.data_ptr(), tuple(w.shape), dt, "kpad", kpad)
+    hit = _wcache.get(key)
+    if hit is not None and _wver.get(key) == w._version:
+        return hit
+    wm = torch.zeros(n, kpad, device=w.device, dtype=dt)
+    wm[:, :k].copy_(ops.cast(w.detach().contiguous(), dt))
+    _wcache[key] = wm
+    _wver[key] = w._version
+    _wsrc[key] = w.detach()  # pins the source storage: its address cannot be reused while cached
+    return wm
+
+
 def wcast_conv(w, k_align=8, cin_pad=None):
     """Conv weight [Cout, Cin, kh, kw] -> GEMM operand [Cout, Kpad] in the compute dtype, column
     order (ky, kx, ci) matching comet_im2col_nhwc / comet_conv2d_nhwc, input channels padded with

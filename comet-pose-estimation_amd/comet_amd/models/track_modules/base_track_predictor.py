@@ -89,14 +89,17 @@ class BaseTrackerPredictor(nn.Module):
         corrdim = self.corr_levels * win
         rows = B * N * S
         corr = torch.empty(rows, corrdim, device=dev, dtype=torch.float32)
-        x = torch.empty(rows, td, device=dev, dtype=F.compute_dtype())
+        # bf16 tokens: rows padded with zeros to a 64-column multiple (664 -> 704, 216 -> 256), so the
+        # update former's input GEMM takes the persistent kernel; the products and sums are unchanged
+        tdp = (td + 63) // 64 * 64 if F.compute_dtype() == torch.bfloat16 else td
+        x = torch.empty(rows, tdp, device=dev, dtype=F.compute_dtype())
         scale = self.stride * down_ratio if down_ratio > 1 else self.stride
         preds = []
         lat = self.latent_dim
         for _ in range(iters):
             ops.corr_sample(pyr, self.corr_radius, track_feats.reshape(rows, C), coords.reshape(rows, 2), corr, 0, B, N, S)
             ops.tracker_tokens(coords, track_feats, lat, corr, corrdim, pos, td, x, rows, S)
-            delta = self.updateformer(x.reshape(B, N, S, td)).reshape(rows, lat + 2)
+            delta = self.updateformer(x.reshape(B, N, S, tdp)).reshape(rows, lat + 2)
             g = ops.layernorm(delta[:, 2:], self.norm.weight, self.norm.bias, eps=self.norm.eps,
                               out_dtype=torch.float32)
             track_feats = _ffeat(g, self.ffeat_updater[0], track_feats.reshape(rows, lat)).reshape(B, N, S, lat)

@@ -154,7 +154,10 @@ class EfficientUpdateFormer(nn.Module):
         attention over (b, t)), so no cat / permute copies are made."""
         B, N0, T, _ = input_tensor.shape
         C = self.hidden_size
-        init = F.linear(input_tensor, self.input_transform.weight, self.input_transform.bias, out_dtype=torch.float32)
+        w_in = self.input_transform.weight
+        if input_tensor.shape[-1] != w_in.shape[1]:  # tokens padded with zero columns to a k-tile multiple
+            w_in = F.wcast_kpad(w_in, input_tensor.shape[-1])
+        init = F.linear(input_tensor, w_in, self.input_transform.bias, out_dtype=torch.float32)
         # every block below starts with a LayerNorm of its input; except for the first ones, those
         # LayerNorms are written by the epilogue of the GEMM that produces the input (the output
         # specs name the consumers), so the token streams move as norm1 pairs (f32, bf16)

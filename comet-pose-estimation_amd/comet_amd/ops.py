@@ -810,8 +810,10 @@ def corr_sample(pyramid, radius, feats, coords, out, col0, B, N, S):
 
 
 def tracker_tokens(coords, feats, latent, corr, corrdim, pos, tdim, x, rows, S):
+    """x [rows, ldx] (ldx = x.stride(0) >= tdim): the update former's input tokens; columns tdim.. are
+    zero padding (the input GEMM's K rounded up to its k-tile)."""
     _chk(L.load().comet_tracker_tokens(dt(x), _p(coords), _p(feats), latent, _p(corr), corr.stride(0), corrdim,
-                                       _p(pos), tdim, _p(x), rows, S, stream()), "tracker_tokens")
+                                       _p(pos), tdim, _p(x), x.stride(0), rows, S, stream()), "tracker_tokens")
 
 
 def coords_update(coords, delta, preds, scale, B, N, S):

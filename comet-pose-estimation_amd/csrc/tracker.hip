@@ -401,7 +401,7 @@ template <typename TO>
 __global__ void __launch_bounds__(256)
 tokens_wave4_kernel(const float* __restrict__ coords, const float* __restrict__ feats, int latent,
                     const float* __restrict__ corr, int64_t ldcorr, int corrdim,
-                    const float* __restrict__ pos, int tdim, TO* __restrict__ x, int64_t rows, int S) {
+                    const float* __restrict__ pos, int tdim, TO* __restrict__ x, int64_t ldx, int64_t rows, int S) {
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= rows) return;
   const int lane = threadIdx.x & 63;
@@ -412,10 +412,16 @@ tokens_wave4_kernel(const float* __restrict__ coords, const float* __restrict__ 
   const float* prow = pos + bn * tdim;
   const float* crow = corr + t * ldcorr;
   const float* frow = feats + t * latent;
-  TO* xrow = x + t * tdim;
+  TO* xrow = x + t * ldx;
   const float dscale = 1000.0f / (float)E;
-  for (int c0 = 4 * lane; c0 < tdim; c0 += 256) {
+  for (int c0 = 4 * lane; c0 < ldx; c0 += 256) {
     float v[4];
+    if (c0 >= tdim) {  // row padding (ldx > tdim: K of the consuming GEMM rounded up to its k-tile)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = 0.f;
+      storen<4>(xrow + c0, v);
+      continue;
+    }
     loadn<4>(prow + c0, v);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -836,17 +842,21 @@ extern "C" int comet_corr_sample(int dtype_fmap, int dtype_feat, const void* con
 
 extern "C" int comet_tracker_tokens(int dtype_out, const float* coords, const float* feats, int latent,
                                     const float* corr, int64_t ldcorr, int corrdim, const float* pos, int tdim,
-                                    void* x, int64_t rows, int S, void* stream) {
-  COMET_CHECK_ARG(coords && feats && corr && pos && x && tdim >= latent * 2 + 2 + corrdim, "comet_tracker_tokens: bad args");
+                                    void* x, int64_t ldx, int64_t rows, int S, void* stream) {
+  COMET_CHECK_ARG(coords && feats && corr && pos && x && tdim >= latent * 2 + 2 + corrdim && ldx >= tdim,
+                  "comet_tracker_tokens: bad args");
   if (rows == 0) return COMET_OK;
   hipStream_t s = as_stream(stream);
   const bool al = ((uintptr_t)x % (dtype_out == COMET_F32 ? 16 : 8)) == 0 && (uintptr_t)pos % 16 == 0;
-  if (tdim % 4 == 0 && al && S > 0 && getenv("COMET_TOKENS_ROWS") == nullptr && getenv("COMET_TOKENS_FLAT") == nullptr) {
+  const bool wave4 = tdim % 4 == 0 && ldx % 4 == 0 && al && S > 0;
+  COMET_CHECK_ARG(ldx == tdim || wave4, "comet_tracker_tokens: padded rows (ldx > tdim) need tdim, ldx % 4 == 0 and "
+                                        "aligned x / pos");
+  if (wave4 && (ldx != tdim || (getenv("COMET_TOKENS_ROWS") == nullptr && getenv("COMET_TOKENS_FLAT") == nullptr))) {
     const unsigned gr = (unsigned)cdiv(rows, 4);
     if (dtype_out == COMET_F32)
-      hipLaunchKernelGGL((tokens_wave4_kernel<float>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (float*)x, rows, S);
+      hipLaunchKernelGGL((tokens_wave4_kernel<float>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (float*)x, ldx, rows, S);
     else
-      hipLaunchKernelGGL((tokens_wave4_kernel<__bf16>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (__bf16*)x, rows, S);
+      hipLaunchKernelGGL((tokens_wave4_kernel<__bf16>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (__bf16*)x, ldx, rows, S);
   } else if (rows < (1ll << 31) && S > 0 && getenv("COMET_TOKENS_FLAT") == nullptr) {
     const RowBlock rb = make_rowblock(rows, tdim);
     const unsigned gr = (unsigned)cdiv(rb.nrows, rb.RB);

@@ -390,10 +390,12 @@ int comet_corr_sample(int dtype_fmap, int dtype_feat, const void* const* pyramid
                       const int* widths, int levels, int radius, int C, const void* feats,
                       const float* coords, float* out, int64_t ldo, int64_t col0, int64_t B, int64_t N,
                       int S, void* stream);
-/* transformer input (base_track_predictor.py:170-221): [flow emb | flows | corr | feats | pad] + pos */
+/* transformer input (base_track_predictor.py:170-221): [flow emb | flows | corr | feats | pad] + pos,
+ * tdim columns at row pitch ldx >= tdim; columns tdim..ldx-1 are written as zeros (rows padded to
+ * the consuming GEMM's 64-deep k-tile; ldx > tdim needs tdim, ldx % 4 == 0 and 16-B aligned pos). */
 int comet_tracker_tokens(int dtype_out, const float* coords, const float* feats, int latent,
                          const float* corr, int64_t ldcorr, int corrdim, const float* pos, int tdim,
-                         void* x, int64_t rows, int S, void* stream);
+                         void* x, int64_t ldx, int64_t rows, int S, void* stream);
 /* coords += delta[:, :2] (frame 0 pinned); preds [B, S, N, 2] = coords * scale (may be NULL) */
 int comet_coords_update(int dtype_delta, float* coords, const void* delta, int64_t ldd, float* preds,
                         float scale, int64_t B, int64_t N, int S, void* stream);

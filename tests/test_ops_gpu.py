@@ -766,6 +766,38 @@ def test_tracker_tokens_row_blocked(dtype, monkeypatch):
     r0 = x1[0].float().cpu() - pos[0].cpu()
     tol = 1e-6 if dtype == torch.float32 else 5e-2
     assert (r0[0:2 * E:2].abs() <= tol).all() and ((r0[1:2 * E:2] - 1).abs() <= tol).all()
+    # rows padded to a 64-column multiple (the bf16 update former's input, round 6): the same tdim
+    # columns, zeros after them
+    tdp = (tdim + 63) // 64 * 64
+    xp = torch.full((rows, tdp), 7.0, device=DEV, dtype=dtype)
+    monkeypatch.delenv("COMET_TOKENS_ROWS")
+    monkeypatch.delenv("COMET_TOKENS_FLAT")
+    ops.tracker_tokens(coords, feats, lat, corr, corrdim, pos, tdim, xp, rows, S)
+    assert torch.equal(xp[:, :tdim], x2) and (xp[:, tdim:] == 0).all()
+
+
+def test_update_former_input_gemm_padded_k():
+    """The update former's input Linear on zero-padded bf16 tokens (K 664 -> 704, 216 -> 256, with
+    the weight's columns padded alike, functional.wcast_kpad) equals the unpadded GEMM within f32
+    summation order and takes the persistent kernel (blocks.py:157, modules.py:119-154)."""
+    from comet_amd import functional as Fn
+    ops = _ops()
+    for M, N, K in [(65536, 384, 664), (65536, 256, 216)]:
+        Kp = (K + 63) // 64 * 64
+        g = torch.Generator(device=DEV).manual_seed(K)
+        x = torch.randn(M, K, device=DEV, generator=g).to(torch.bfloat16)
+        xp = torch.zeros(M, Kp, device=DEV, dtype=torch.bfloat16)
+        xp[:, :K] = x
+        w = torch.nn.Parameter(torch.randn(N, K, device=DEV, generator=g) * K ** -0.5)
+        b = torch.randn(N, device=DEV, generator=g)
+        with torch.no_grad(), Fn.precision(torch.bfloat16):
+            y = Fn.linear(x, w, b, out_dtype=torch.float32)
+            yp = Fn.linear(xp, Fn.wcast_kpad(w, Kp), b, out_dtype=torch.float32)
+        assert tuple(ops._PLAN)[0] == 3, f"padded K {Kp}: expected the persistent plan, got {tuple(ops._PLAN)}"
+        ref = x.double() @ w.detach().to(torch.bfloat16).double().t() + b.double()
+        for out in (y, yp):
+            assert ((out.double() - ref).abs() <= 1e-5 * ref.abs() + 2e-5 * K ** 0.5).all()
+        Fn.invalidate_weight_cache([w])
 
 
 def _corr_ref(pyr, radius, feats, coords, B, N, S):
