@@ -3,6 +3,8 @@
 //
 // Reference sites: train_eval_func_new_cp5.py:790-801 (backward, clip_grad_norm_(1.0),
 // optimizer.step), train_util.py:311-332 (AdamW over camera_predictor.parameters()).
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace comet {
@@ -361,7 +363,10 @@ extern "C" int comet_act_bwd_colsum(int act, int dtype_pre, const void* pre, int
   }
   if (rows == 0) return COMET_OK;
   const int64_t cblocks = cdiv(cols, 256);
-  int64_t rblocks = cdiv(2048, cblocks);                 // ~2048 workgroups
+  // ~4096 workgroups (2-3 % faster than 2048 on the 73856-row f32 and bf16 shapes, tools/tail_ab.py,
+  // profiles/r06_tail/tail_ab.txt; 1024: 2-7 % slower); COMET_COLSUM_WGS overrides (measurement)
+  const char* cw = getenv("COMET_COLSUM_WGS");
+  int64_t rblocks = cdiv(cw != nullptr && atoll(cw) > 0 ? atoll(cw) : 4096, cblocks);
   int64_t chunk = cdiv(rows, rblocks);
   if (chunk < 64) chunk = 64;
   rblocks = cdiv(rows, chunk);
