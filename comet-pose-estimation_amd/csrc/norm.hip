@@ -189,6 +189,59 @@ ln_fwd_vec_kernel(const TX* __restrict__ x, const float* __restrict__ w, const f
   }
 }
 
+// Narrow rows (cols <= 8 x CH: the tracker's GroupNorm(1, 32) rows): RPW rows per wave, 64 / RPW
+// lanes per row, one CH-chunk per lane. The sums are the segmented tail of wave_sum's
+// butterfly (offsets 32 / RPW .. 1); in the one-row-per-wave kernel the larger offsets only add the
+// idle lanes' zeros, so mean, variance and outputs are bit-identical to ln_fwd_vec_kernel.
+template <typename TX, typename TY, int CH, int RPW>
+__global__ void __launch_bounds__(256)
+ln_fwd_narrow_kernel(const TX* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                     TY* __restrict__ y, __bf16* __restrict__ y2, float* __restrict__ mean_out,
+                     float* __restrict__ rstd_out, int64_t rows, int cols, int64_t ldx, int64_t ldy,
+                     int64_t ldy2, float eps, int relu) {
+  constexpr int LPR = 64 / RPW;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const int c0 = (lane % LPR) * CH;
+  const bool live = row < rows && c0 < cols;
+  float v[CH];
+#pragma unroll
+  for (int e = 0; e < CH; ++e) v[e] = 0.f;
+  if (live) loadn<CH>(x + row * ldx + c0, v);
+  auto seg_sum = [](float t) {
+#pragma unroll
+    for (int off = LPR / 2; off >= 1; off >>= 1) t += __shfl_xor(t, off, 64);
+    return t;
+  };
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < CH; ++e) s += v[e];
+  const float mean = seg_sum(s) / cols;
+  float q = 0.f;
+  if (live) {
+#pragma unroll
+    for (int e = 0; e < CH; ++e) { const float d = v[e] - mean; q += d * d; }
+  }
+  const float var = seg_sum(q) / cols;
+  const float rstd = rsqrtf(var + eps);
+  if (!live) return;
+  float o[CH];
+#pragma unroll
+  for (int e = 0; e < CH; ++e) {
+    float t = (v[e] - mean) * rstd;
+    if (w) t = t * w[c0 + e];
+    if (b) t = t + b[c0 + e];
+    if (relu) t = t > 0.f ? t : 0.f;
+    o[e] = t;
+  }
+  if (y) storen<CH>(y + row * ldy + c0, o);
+  if (y2) storen<CH>(y2 + row * ldy2 + c0, o);
+  if (c0 == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+}
+
 // Persistent-row form of ln_fwd_vec_kernel: each wave walks rows wave_id, wave_id + waves, ... and
 // issues the next row's loads before reducing / storing the current one (a one-row-per-wave block
 // lives mostly in load latency, so the short blocks held the forward near 3.8 TB/s).
@@ -651,9 +704,23 @@ extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, cons
     const bool flat = rows <= 2 * 2048 * 4 || getenv("COMET_LN_FLAT") != nullptr;
     const int64_t iters = cdiv(rows, 2048 * 4);
     const dim3 grid_rows((unsigned)cdiv(cdiv(rows, iters), 4));
+    // narrow rows: 8 rows per wave for rows of <= 8 lanes x CH (65536 x 32 f32: 13.5 vs 16.2 us; at 32
+    // lanes per row the persistent-row kernel's prefetch wins, 18.3 vs 23.8 us at 65536 x 128,
+    // profiles/r06_tail/tail_ab_narrow.txt); COMET_LN_NO_NARROW=1: one row per wave
+    const int ch_n = (dtype_x == COMET_F32 || (y && dtype_y == COMET_F32)) ? 4 : 8;
+    const int lanes = (int)cdiv(cols, ch_n);
+    const int rpw_n = lanes <= 8 ? 8 : 1;
+    const bool narrow = rpw_n > 1 && getenv("COMET_LN_NO_NARROW") == nullptr;
+#define LNN(TX, TY, CH)                                                                                        \
+  do {                                                                                                         \
+    const dim3 gn((unsigned)cdiv(rows, 4 * rpw_n));                                                            \
+    hipLaunchKernelGGL((ln_fwd_narrow_kernel<TX, TY, CH, 8>), gn, dim3(256), 0, s, (const TX*)x, weight,        \
+                       bias, (TY*)y, (__bf16*)y2, mean, rstd, rows, (int)cols, ldx, ldy, ldy2, eps, relu);     \
+  } while (0)
 #define LNV(TX, TY, CH, NK)                                                                                    \
   do {                                                                                                         \
-    if (flat)                                                                                                  \
+    if (narrow && NK == 1) LNN(TX, TY, CH);                                                                    \
+    else if (flat)                                                                                             \
       hipLaunchKernelGGL((ln_fwd_vec_kernel<TX, TY, CH, NK>), grid, dim3(256), 0, s, (const TX*)x, weight,      \
                          bias, (TY*)y, (__bf16*)y2, mean, rstd, rows, (int)cols, ldx, ldy, ldy2, eps, relu);   \
     else                                                                                                       \
@@ -677,6 +744,7 @@ extern "C" int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, cons
 #undef LNV2
 #undef LNV_CH
 #undef LNV
+#undef LNN
     COMET_CHECK_LAUNCH("comet_layernorm_fwd");
     return COMET_OK;
   }

@@ -1241,6 +1241,33 @@ def test_conv1x1_resize_pool_fused(c, n, hw, o, ups):
     assert torch.equal(q, ops.avgpool2_nhwc(p_ref)), "second pyramid level differs"
 
 
+@pytest.mark.parametrize("cols", [8, 32, 64])
+@pytest.mark.parametrize("dts", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                 (torch.bfloat16, torch.bfloat16)])
+def test_layernorm_narrow_rows_bit_identical(cols, dts, monkeypatch):
+    """The several-rows-per-wave LayerNorm for narrow rows (the tracker's GroupNorm(1, 32),
+    base_track_predictor.py:81,238; bf16 rows up to 64 columns) equals the one-row-per-wave kernel
+    (COMET_LN_NO_NARROW=1) bit for bit -- outputs, the bf16 copy, mean and rstd -- with affine
+    weights, relu, and a row count that does not fill the last wave; and matches torch's f32 LN."""
+    ops = _ops()
+    tx, ty = dts
+    g = torch.Generator(device=DEV).manual_seed(cols)
+    rows = 1001
+    x = (torch.randn(rows, cols, device=DEV, generator=g) * 3 + 1).to(tx)
+    w = torch.randn(cols, device=DEV, generator=g)
+    b = torch.randn(cols, device=DEV, generator=g)
+    outs = []
+    for narrow in (True, False):
+        if not narrow:
+            monkeypatch.setenv("COMET_LN_NO_NARROW", "1")
+        outs.append(ops.layernorm(x, w, b, eps=1e-5, out_dtype=ty, stats=True, dual=True, relu=True))
+    for a, r in zip(outs[0], outs[1]):
+        assert torch.equal(a, r)
+    ref = torch.relu(torch.nn.functional.layer_norm(x.float(), (cols,), w, b, eps=1e-5))
+    tol = 1e-5 if ty == torch.float32 else 1e-2
+    assert (outs[0][0].float() - ref).abs().max().item() <= tol * (1 + ref.abs().max().item())
+
+
 def test_cast_multi_and_weight_cache_refresh():
     """comet_cast_multi_f32_bf16 equals torch's RNE .to(bfloat16) bit for bit (aligned and
     unaligned views, > 48 tensors); refresh_weight_cache re-casts cached copies in place after

@@ -25,7 +25,14 @@ def main():
     g = torch.randn(73856, 768, device="cuda")
     gb = torch.randn(73856, 2304, device="cuda").to(torch.bfloat16)
     db = torch.empty(2304, device="cuda")
+    x32 = torch.randn(65536, 32, device="cuda")
+    x128 = torch.randn(65536, 128, device="cuda")
+    w32, w128 = torch.randn(32, device="cuda"), torch.randn(128, device="cuda")
     cases = {
+        "layernorm f32 65536 x 32 (tracker GroupNorm(1, 32))": (
+            lambda: ops.layernorm(x32, w32, w32, eps=1e-5, out_dtype=torch.float32), 65536 * 32 * 8),
+        "layernorm f32 65536 x 128 (tracker GroupNorm(1, 128))": (
+            lambda: ops.layernorm(x128, w128, w128, eps=1e-5, out_dtype=torch.float32), 65536 * 128 * 8),
         "layernorm f32 -> bf16 74368 x 768 (DINOv2 norm1/2)": (
             lambda: ops.layernorm(x, w, b, eps=1e-6, out_dtype=torch.bfloat16), 74368 * 768 * 6),
         "act_bwd_colsum f32 -> bf16 + colsum 73856 x 768": (
