@@ -131,6 +131,73 @@ corr_kernel(PyrTab tab, int levels, int radius, const TT* __restrict__ feats, co
   }
 }
 
+// corr_kernel with one wave per track row instead of one workgroup (the fine tracker: C = 32, r = 3,
+// a 10 x 10 grid per level): no workgroup barriers, all 64 lanes busy on the grid's dot products
+// (LPP = 2 lanes per pixel, 32 pixels per pass) and 49 of 64 on the window samples, four rows per
+// workgroup. Per pixel and per sample the arithmetic -- the lane's 16-channel partial sums, the xor
+// shuffle over the LPP lanes, the bilinear weights -- is corr_kernel's, so the outputs are bit-identical.
+// 65536 fine rows: 184 vs 231 us (profiles/r06_tail/corr_wave_ab.txt; issuing all four passes' loads
+// first measured 262 us: the extra registers cost more occupancy than the loads gained).
+template <typename TF, typename TT, int C>
+__global__ void __launch_bounds__(256)
+corr_wave_kernel(PyrTab tab, int levels, int radius, const TT* __restrict__ feats, const float* __restrict__ coords,
+                 float* __restrict__ out, int64_t ldo, int64_t col0, int64_t N, int S, float inv_sqrt_c, int64_t T) {
+  constexpr int G = 16, LPP = C / 16, PPW = 64 / LPP;
+  __shared__ float dots_w[4][G * G];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t t = (int64_t)blockIdx.x * 4 + wv;  // (b*N + n)*S + s
+  if (t >= T) return;  // whole waves; no workgroup barrier below
+  const int s = (int)(t % S);
+  const int64_t b = (t / S) / N;
+  float* dots = dots_w[wv];
+  const int sub = lane % LPP, pslot = lane / LPP;
+  float fr[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) fr[e] = to_f32(feats[t * C + sub * 16 + e]);
+  const float cx = coords[t * 2], cy = coords[t * 2 + 1];
+  const int win = 2 * radius + 1, gs = 2 * radius + 4;
+  float* orow = out + t * ldo + col0;
+  for (int l = 0; l < levels; ++l) {
+    const int H = tab.h[l], W = tab.w[l];
+    const TF* fm = reinterpret_cast<const TF*>(tab.p[l]) + (b * S + s) * (int64_t)H * W * C;
+    const float scl = 1.f / (float)(1 << l);
+    const float xl = cx * scl, yl = cy * scl;
+    const int gx0 = (int)floorf(xl) - radius - 1, gy0 = (int)floorf(yl) - radius - 1;
+    __builtin_amdgcn_wave_barrier();  // the previous level's samples read dots before it is rewritten
+    for (int p0 = 0; p0 < gs * gs; p0 += PPW) {
+      const int p = p0 + pslot;
+      const int px = gx0 + p % gs, py = gy0 + p / gs;
+      float acc = 0.f;
+      if (p < gs * gs && px >= 0 && px < W && py >= 0 && py < H) {
+        const TF* pix = fm + ((int64_t)py * W + px) * C + sub * 16;
+        float a[8], c8[8];
+        load8(pix, a);
+        load8(pix + 8, c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += fr[e] * a[e] + fr[8 + e] * c8[e];
+      }
+#pragma unroll
+      for (int o = LPP / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (sub == 0 && p < gs * gs) dots[(p / gs) * G + (p % gs)] = acc * inv_sqrt_c;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's dot products are in LDS
+    __builtin_amdgcn_wave_barrier();
+    for (int k = lane; k < win * win; k += 64) {
+      const int i = k / win, j = k % win;
+      const float ix = src_index(xl + (float)(i - radius), W, false);
+      const float iy = src_index(yl + (float)(j - radius), H, false);
+      const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+      const float wnw = ((float)(x0 + 1) - ix) * ((float)(y0 + 1) - iy), wne = (ix - (float)x0) * ((float)(y0 + 1) - iy);
+      const float wsw = ((float)(x0 + 1) - ix) * (iy - (float)y0), wse = (ix - (float)x0) * (iy - (float)y0);
+      auto D = [&](int x, int y) -> float {
+        const int gx = x - gx0, gy = y - gy0;
+        return (gx >= 0 && gx < gs && gy >= 0 && gy < gs) ? dots[gy * G + gx] : 0.f;
+      };
+      orow[l * win * win + k] = D(x0, y0) * wnw + D(x0 + 1, y0) * wne + D(x0, y0 + 1) * wsw + D(x0 + 1, y0 + 1) * wse;
+    }
+  }
+}
+
 // The same CorrBlock step on the matrix cores, for bf16 maps with C = 128 (the coarse tracker:
 // 512 tracks per frame on a 64 x 64 map). The tracks of one frame read overlapping windows, so
 // the dot products are formed as dense MFMA tiles (16 map pixels x 16 tracks x 32 channels) over
@@ -829,6 +896,15 @@ extern "C" int comet_corr_sample(int dtype_fmap, int dtype_feat, const void* con
                                     radius, (const float*)feats, coords, out, ldo, col0, (int)N, S, (int)frames, isc, sort)
     if (!occ3) CM(2, 4); else if (ring >= 4) CM(4, 1); else if (ring == 3) CM(3, 1); else CM(2, 1);
 #undef CM
+    COMET_CHECK_LAUNCH("comet_corr_sample");
+    return COMET_OK;
+  }
+  if (C == 32 && std::getenv("COMET_CORR_BLOCK") == nullptr) {
+    // the fine tracker: one wave per track row (corr_wave_kernel; COMET_CORR_BLOCK=1: a workgroup per row)
+#define CW(TF) hipLaunchKernelGGL((corr_wave_kernel<TF, float, 32>), dim3((unsigned)((T + 3) / 4)), dim3(256), 0, s, tab, \
+                                  levels, radius, (const float*)feats, coords, out, ldo, col0, N, S, isc, T)
+    if (dtype_fmap == COMET_F32) CW(float); else CW(__bf16);
+#undef CW
     COMET_CHECK_LAUNCH("comet_corr_sample");
     return COMET_OK;
   }

@@ -852,6 +852,38 @@ def test_corr_sample_vs_f64(C, radius, dtype):
     assert (out[:, :2] == 7.0).all() and (out[:, 2 + levels * win * win:] == 7.0).all()
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_corr_sample_wave_per_row_bit_identical(dtype, monkeypatch):
+    """The fine tracker's correlation (C = 32, radius 3, 3 levels on 31 x 31 patch maps and their
+    pools): the one-wave-per-row kernel (default) equals the one-workgroup-per-row kernel
+    (COMET_CORR_BLOCK=1) bit for bit, for a row count that does not fill the last workgroup, tracks
+    near and beyond the border and a NaN track; and both match the f64 restatement."""
+    ops = _ops()
+    B, N, S, levels, radius, C = 1, 37, 3, 3, 3, 32
+    sizes = [31, 15, 7]
+    pyr = [_rand(B * S, sizes[l], sizes[l], C, seed=340 + l).to(dtype).to(DEV) for l in range(levels)]
+    rows = B * N * S
+    feats = _rand(rows, C, seed=350)
+    coords = torch.rand(rows, 2, generator=torch.Generator().manual_seed(351)) * 39 - 4
+    coords[7] = float("nan")
+    win = 2 * radius + 1
+    outs = []
+    for block in (False, True):
+        if block:
+            monkeypatch.setenv("COMET_CORR_BLOCK", "1")
+        o = torch.full((rows, levels * win * win + 2), 7.0, device=DEV)
+        ops.corr_sample(pyr, radius, feats.to(DEV), coords.to(DEV), o, 1, B, N, S)
+        outs.append(o)
+    assert torch.equal(torch.nan_to_num(outs[0], nan=123.0), torch.nan_to_num(outs[1], nan=123.0))
+    ok = torch.ones(rows, dtype=torch.bool)
+    ok[7] = False
+    cref = coords.clone()
+    cref[7] = 0.0  # (the f64 restatement indexes with the coordinates; the NaN row is not compared)
+    ref = _corr_ref(pyr, radius, feats, cref, B, N, S)
+    _close(outs[0][ok.to(DEV), 1:1 + levels * win * win], ref[ok], 1e-4, 1e-4, "corr wave C=32")
+    assert (outs[0][:, :1] == 7.0).all() and (outs[0][:, 1 + levels * win * win:] == 7.0).all()
+
+
 @pytest.mark.parametrize("layout", ["uniform", "clustered", "outside"])
 def test_corr_sample_mfma_vs_f64(layout):
     """The matrix-core CorrBlock path (bf16 maps, C = 128, >= 16 tracks per frame: the coarse

@@ -28,7 +28,13 @@ def main():
     x32 = torch.randn(65536, 32, device="cuda")
     x128 = torch.randn(65536, 128, device="cuda")
     w32, w128 = torch.randn(32, device="cuda"), torch.randn(128, device="cuda")
+    fpyr = [torch.randn(65536, n, n, 32, device="cuda").to(torch.bfloat16) for n in (31, 15, 7)]
+    ffeat = torch.randn(65536, 32, device="cuda")
+    fco = torch.rand(65536, 2, device="cuda") * 31
+    fout = torch.empty(65536, 147, device="cuda")
     cases = {
+        "corr_sample fine (65536 rows, C 32, r 3, 3 levels)": (
+            lambda: ops.corr_sample(fpyr, 3, ffeat, fco, fout, 0, 4096, 1, 16), 65536 * (147 * 4 + 32 * 4 + 8 + 3 * 100 * 64)),
         "layernorm f32 65536 x 32 (tracker GroupNorm(1, 32))": (
             lambda: ops.layernorm(x32, w32, w32, eps=1e-5, out_dtype=torch.float32), 65536 * 32 * 8),
         "layernorm f32 65536 x 128 (tracker GroupNorm(1, 128))": (
