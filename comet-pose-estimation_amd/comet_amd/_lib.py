@@ -109,9 +109,9 @@ SIGNATURES = {
     "comet_layernorm_fwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64,
                                    c_i64, _F, _INT, c_vp]),
     "comet_layernorm_bwd": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, _INT, c_vp, c_vp, c_vp, c_i64, c_i64,
-                                   _INT, c_vp, c_vp]),
+                                   _INT, c_vp]),
     "comet_layernorm_bwd_res": (_INT, [_INT, _INT, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64,
-                                       c_vp, c_vp]),
+                                       c_vp]),
     "comet_attention_bwd": (_INT, [ctypes.POINTER(AttnBwdArgs), c_vp]),
     "comet_attention_fwd": (_INT, [ctypes.POINTER(AttnArgs), c_vp]),
     "comet_attn_probs": (_INT, [_INT, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, _F, c_vp]),

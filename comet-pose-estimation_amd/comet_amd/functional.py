@@ -150,30 +150,7 @@ def _vec8(t):
     return t.is_contiguous() and t.shape[-1] % 8 == 0 and t.data_ptr() % 32 == 0
 
 
-def _bf16_side(t):
-    """The bf16 copy of gradient t that the LayerNorm backward producing it wrote in the same pass
-    (_attach_bf16), if still current: an in-place update of t (autograd accumulating another gradient
-    into it) bumps its version and the copy is ignored."""
-    side = getattr(t, "_comet_bf16", None)
-    if side is None or side[1] != t._version or side[0].shape != t.shape:
-        return None
-    return side[0]
-
-
-def _attach_bf16(t, t16):
-    t._comet_bf16 = (t16, t._version)
-    return t
-
-
-def _want_bf16_side(x, cdt):
-    """An f32 LayerNorm input whose gradient feeds a bf16 Linear backward (the residual stream of the
-    camera head's blocks): its LayerNorm backward writes the bf16 copy the Linear's GEMMs and bias
-    gradient read (one f32 read + bf16 write pass fewer per block)."""
-    return (cdt == torch.bfloat16 and x.dtype == torch.float32 and x.shape[-1] % 8 == 0
-            and x.numel() // x.shape[-1] >= 4096 and not os.environ.get("COMET_NO_BF16_SIDE"))
-
-
-def _linear_bwd(x2, wc, dy2, act, aux, need_dx, need_dw, need_db, dx_dtype, dy16=None):
+def _linear_bwd(x2, wc, dy2, act, aux, need_dx, need_dw, need_db, dx_dtype):
     """dy2 [M, N] (dL/d output) -> dx [M, K] (dx_dtype), dW [N, K] f32, db [N] f32.
     bf16 compute: act', the bf16 GEMM operand and the bias gradient in one pass
     (comet_act_bwd_colsum); x2 was saved in bf16 by the forward."""
@@ -184,13 +161,7 @@ def _linear_bwd(x2, wc, dy2, act, aux, need_dx, need_dw, need_db, dx_dtype, dy16
     if cdt == torch.bfloat16 and _vec8(dy2) and (aux is None or _vec8(aux)):
         if need_db:
             db = torch.empty(N, device=dy2.device, dtype=torch.float32)
-        if act == L.ACT_NONE and dy16 is not None:
-            # the bf16 operand written by the LayerNorm backward that produced dy2: only the bias
-            # gradient pass remains (it sums the same rounded values)
-            dpre = dy16
-            if need_db:
-                ops.act_bwd_colsum(L.ACT_NONE, None, dy16, dbias=db, want_out=False)
-        elif act != L.ACT_NONE or dy2.dtype != torch.bfloat16:
+        if act != L.ACT_NONE or dy2.dtype != torch.bfloat16:
             # one pass: act' (if any), bf16 GEMM operand, bias gradient
             dpre = ops.act_bwd_colsum(act, aux, dy2, out_dtype=torch.bfloat16, dbias=db)
         else:
@@ -244,10 +215,8 @@ class _Linear(torch.autograd.Function):
         wc = wcast(w, ctx.cdt)
         # dx straight in the input's dtype (the reference's autocast grad of a bf16 tensor is bf16)
         dx_dtype = ctx.xdtype if ctx.cdt == torch.bfloat16 else torch.float32
-        side = _bf16_side(dy)
         dx, dw, db = _linear_bwd(x2, wc, dy2, ctx.act, aux, ctx.needs_input_grad[0], ctx.needs_input_grad[1],
-                                 ctx.has_b and ctx.needs_input_grad[2], dx_dtype,
-                                 dy16=side.reshape(-1, N) if side is not None else None)
+                                 ctx.has_b and ctx.needs_input_grad[2], dx_dtype)
         if dx is not None:
             dx = dx.reshape(ctx.shape)
             if dx.dtype != ctx.xdtype:
@@ -303,12 +272,10 @@ class _Mlp(torch.autograd.Function):
         # fc2: the bf16 operand of its two GEMMs and its bias gradient in one pass, then dW2 (its dX
         # is the fused GEMM below)
         db2 = torch.empty(N, device=dy.device, dtype=torch.float32) if ctx.has_b2 and ni[4] else None
-        side = _bf16_side(dy)
-        if dy2.dtype == torch.bfloat16 or side is not None:
-            # bf16 gradient, or the bf16 copy its LayerNorm backward wrote: only the bias-gradient pass
-            dpre2 = dy2 if side is None else side.reshape(-1, N)
+        if dy2.dtype == torch.bfloat16:
+            dpre2 = dy2
             if db2 is not None:
-                ops.act_bwd_colsum(L.ACT_NONE, None, dpre2, dbias=db2, want_out=False)
+                ops.act_bwd_colsum(L.ACT_NONE, None, dy2, dbias=db2, want_out=False)
         else:
             dpre2 = ops.act_bwd_colsum(L.ACT_NONE, None, dy2, out_dtype=torch.bfloat16, dbias=db2)
         _, dw2, _ = _linear_bwd(h, wc2, dpre2, L.ACT_NONE, None, False, ni[3], False, torch.bfloat16)
@@ -378,7 +345,6 @@ class _LayerNormDual(torch.autograd.Function):
     def forward(ctx, x, eps):
         y, y16, mean, rstd = ops.layernorm(x, None, None, eps=eps, out_dtype=torch.float32, stats=True, dual=True)
         ctx.save_for_backward(x, mean, rstd)
-        ctx.cdt = compute_dtype()
         return y, y16
 
     @staticmethod
@@ -388,9 +354,8 @@ class _LayerNormDual(torch.autograd.Function):
             dy, dy16 = dy16, None
         if dy is None:
             return None, None
-        dx16 = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16) if _want_bf16_side(x, ctx.cdt) else None
-        dx = ops.layernorm_bwd(x, dy, mean, rstd, dy2=dy16, dx_dtype=x.dtype, dx16=dx16)
-        return (_attach_bf16(dx, dx16) if dx16 is not None else dx), None
+        dx = ops.layernorm_bwd(x, dy, mean, rstd, dy2=dy16, dx_dtype=x.dtype)
+        return dx, None
 
 
 class _ResLayerNorm(torch.autograd.Function):
@@ -402,7 +367,6 @@ class _ResLayerNorm(torch.autograd.Function):
     def forward(ctx, x, eps):
         y, mean, rstd = ops.layernorm(x, eps=eps, out_dtype=compute_dtype(), stats=True)
         ctx.save_for_backward(x, mean, rstd)
-        ctx.cdt = compute_dtype()
         return x.view_as(x), y
 
     @staticmethod
@@ -413,9 +377,7 @@ class _ResLayerNorm(torch.autograd.Function):
         if dres is None:
             return ops.layernorm_bwd(x, dy, mean, rstd, dx_dtype=x.dtype), None
         if x.dtype == torch.float32 and x.shape[-1] % 8 == 0:
-            dx16 = torch.empty(x.shape, device=x.device, dtype=torch.bfloat16) if _want_bf16_side(x, ctx.cdt) else None
-            dx = ops.layernorm_bwd_res(x, dy, dres, mean, rstd, dx16=dx16)
-            return (_attach_bf16(dx, dx16) if dx16 is not None else dx), None
+            return ops.layernorm_bwd_res(x, dy, dres, mean, rstd), None
         return ops.layernorm_bwd(x, dy, mean, rstd, dx_dtype=x.dtype) + dres, None
 
 

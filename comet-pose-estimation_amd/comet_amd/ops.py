@@ -363,9 +363,8 @@ def layernorm(x, weight=None, bias=None, eps=1e-5, out_dtype=None, stats=False, 
 
 
 def layernorm_bwd(x, dy, mean, rstd, weight=None, dweight=None, dbias=None, dx=None, accumulate=False, dy2=None,
-                  dx_dtype=torch.float32, dx16=None):
-    """dx = LN backward of dy (+ dy2, bf16); dweight/dbias accumulated; dx16 (bf16, optional) receives
-    a rounded copy of dx from the same pass."""
+                  dx_dtype=torch.float32):
+    """dx = LN backward of dy (+ dy2, bf16); dweight/dbias accumulated."""
     C = x.shape[-1]
     rows = x.numel() // C
     xc = x.contiguous()
@@ -376,19 +375,18 @@ def layernorm_bwd(x, dy, mean, rstd, weight=None, dweight=None, dbias=None, dx=N
         accumulate = False
     L.check(L.load().comet_layernorm_bwd(dt(xc), dt(dyc), _p(xc), _p(dyc), _p(dy2c), _p(mean), _p(rstd),
                                          _p(weight), dt(dx), _p(dx), _p(dweight), _p(dbias), rows, C,
-                                         int(accumulate), _p(dx16), stream()), "layernorm_bwd")
+                                         int(accumulate), stream()), "layernorm_bwd")
     return dx
 
 
-def layernorm_bwd_res(x, dy, dres, mean, rstd, weight=None, dweight=None, dbias=None, dx16=None):
-    """dx (f32) = dres + LN backward of dy (x + f(LN(x)) without a separate gradient add); dx16 (bf16,
-    optional) receives a rounded copy of dx from the same pass."""
+def layernorm_bwd_res(x, dy, dres, mean, rstd, weight=None, dweight=None, dbias=None):
+    """dx (f32) = dres + LN backward of dy (x + f(LN(x)) without a separate gradient add)."""
     C = x.shape[-1]
     rows = x.numel() // C
     xc, dyc, drc = x.contiguous(), dy.contiguous(), dres.contiguous().float()
     dx = torch.empty(x.shape, device=x.device, dtype=torch.float32)
     L.check(L.load().comet_layernorm_bwd_res(dt(xc), dt(dyc), _p(xc), _p(dyc), _p(drc), _p(mean), _p(rstd),
-                                             _p(weight), _p(dx), _p(dweight), _p(dbias), rows, C, _p(dx16), stream()),
+                                             _p(weight), _p(dx), _p(dweight), _p(dbias), rows, C, stream()),
             "layernorm_bwd_res")
     return dx
 

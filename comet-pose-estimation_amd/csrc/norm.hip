@@ -329,8 +329,7 @@ __global__ void __launch_bounds__(256)
 ln_bwd_vec_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const __bf16* __restrict__ dy2,
                   const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w,
                   TO* __restrict__ dx, float* __restrict__ dw, float* __restrict__ db, int64_t rows, int cols,
-                  int accum, const float* __restrict__ dres = nullptr, int rpw = LN_RPW,
-                  __bf16* __restrict__ dx16 = nullptr) {
+                  int accum, const float* __restrict__ dres = nullptr, int rpw = LN_RPW) {
   __shared__ float red[2][4][1024];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float gw[NK][CH], gb[NK][CH], wv[NK][CH];
@@ -399,8 +398,6 @@ ln_bwd_vec_kernel(const TX* __restrict__ x, const TD* __restrict__ dy, const __b
         for (int e = 0; e < CH; ++e) o[e] += r[e];
       }
       storen<CH>(p, o);
-      // the bf16 copy of dx for the consumer's GEMMs (the bias gradient then sums these values)
-      if (dx16) storen<CH>(dx16 + row * cols + c0, o);
     }
   }
   if (!dw && !db) return;
@@ -780,20 +777,19 @@ static int ln_bwd_rpw(const float* dweight, const float* dbias) {
 extern "C" int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy, const void* dy2,
                                    const float* mean, const float* rstd, const float* weight,
                                    int dtype_dx, void* dx, float* dweight, float* dbias, int64_t rows,
-                                   int64_t cols, int dx_accumulate, void* dx16, void* stream) {
+                                   int64_t cols, int dx_accumulate, void* stream) {
   COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_bwd: cols must be in [1,1024]");
   COMET_CHECK_ARG(x && dy && mean && rstd && dx, "comet_layernorm_bwd: null pointer");
   if (rows == 0) return COMET_OK;
   const int rpw = ln_bwd_rpw(dweight, dbias);
   dim3 grid((unsigned)cdiv(rows, 4 * rpw));
   hipStream_t s = as_stream(stream);
-  const bool vec = cols % 8 == 0 && a32(x) && a32(dy) && a32(dy2) && a32(dx) && a32(dx16);
-  COMET_CHECK_ARG(dx16 == nullptr || vec, "comet_layernorm_bwd: the bf16 copy needs cols % 8 == 0 and 32-B aligned rows");
+  const bool vec = cols % 8 == 0 && a32(x) && a32(dy) && a32(dy2) && a32(dx);
   if (vec) {
 #define LBV(TX, TD, TO, CH, NK)                                                                           \
   hipLaunchKernelGGL((ln_bwd_vec_kernel<TX, TD, TO, CH, NK>), grid, dim3(256), 0, s, (const TX*)x, (const TD*)dy, \
                      (const __bf16*)dy2, mean, rstd, weight, (TO*)dx, dweight, dbias, rows, (int)cols, dx_accumulate, \
-                     nullptr, rpw, (__bf16*)dx16)
+                     nullptr, rpw)
 #define LBV_CH(TX, TD, TO, CH)                                                                             \
   do {                                                                                                     \
     const int nk = (int)cdiv(cols, 64 * CH);                                                               \
@@ -897,11 +893,10 @@ extern "C" int comet_instnorm_nhwc(int dtype, const void* x, const void* res, vo
 // 342-343): dx = dres + LN backward of dy in one pass (no separate gradient add).
 extern "C" int comet_layernorm_bwd_res(int dtype_x, int dtype_dy, const void* x, const void* dy, const float* dres,
                                        const float* mean, const float* rstd, const float* weight, float* dx,
-                                       float* dweight, float* dbias, int64_t rows, int64_t cols, void* dx16,
-                                       void* stream) {
+                                       float* dweight, float* dbias, int64_t rows, int64_t cols, void* stream) {
   COMET_CHECK_ARG(cols > 0 && cols <= 64 * LN_MAXV, "comet_layernorm_bwd_res: cols must be in [1,1024]");
   COMET_CHECK_ARG(x && dy && dres && mean && rstd && dx, "comet_layernorm_bwd_res: null pointer");
-  COMET_CHECK_ARG(cols % 8 == 0 && a32(x) && a32(dy) && a32(dres) && a32(dx) && a32(dx16),
+  COMET_CHECK_ARG(cols % 8 == 0 && a32(x) && a32(dy) && a32(dres) && a32(dx),
                   "comet_layernorm_bwd_res: needs cols % 8 == 0 and 32-B aligned rows");
   if (rows == 0) return COMET_OK;
   const int rpw = ln_bwd_rpw(dweight, dbias);
@@ -909,8 +904,7 @@ extern "C" int comet_layernorm_bwd_res(int dtype_x, int dtype_dy, const void* x,
   hipStream_t s = as_stream(stream);
 #define LBR(TX, TD, NK)                                                                                          \
   hipLaunchKernelGGL((ln_bwd_vec_kernel<TX, TD, float, 4, NK>), grid, dim3(256), 0, s, (const TX*)x, (const TD*)dy, \
-                     (const __bf16*)nullptr, mean, rstd, weight, dx, dweight, dbias, rows, (int)cols, 0, dres, rpw, \
-                     (__bf16*)dx16)
+                     (const __bf16*)nullptr, mean, rstd, weight, dx, dweight, dbias, rows, (int)cols, 0, dres, rpw)
 #define LBR_NK(TX, TD)                                                            \
   do {                                                                            \
     const int nk = (int)cdiv(cols, 64 * 4);                                       \

@@ -162,18 +162,16 @@ int comet_layernorm_fwd(int dtype_x, int dtype_y, const void* x, const float* we
 /* y2 (bf16, may be NULL; y may be NULL when y2 is given): a second copy of the output for the GEMM
  * that consumes it (AttnBlock: the normed x is both the in_proj input and the residual).
  * dx (dtype_dx) = LN backward of dy + dy2 (dy2 bf16, may be NULL); dweight/dbias (f32) are
- * ACCUMULATED (+=) when non-NULL. dx_accumulate != 0 adds into dx instead of overwriting. dx16
- * (bf16 [rows, cols], may be NULL): a rounded copy of dx, written by the same pass, for the GEMMs of
- * the Linear that produced x (round 6; cols % 8 == 0, 32-B aligned rows). */
+ * ACCUMULATED (+=) when non-NULL. dx_accumulate != 0 adds into dx instead of overwriting. */
 int comet_layernorm_bwd(int dtype_x, int dtype_dy, const void* x, const void* dy, const void* dy2,
                         const float* mean, const float* rstd, const float* weight,
                         int dtype_dx, void* dx, float* dweight, float* dbias, int64_t rows, int64_t cols,
-                        int dx_accumulate, void* dx16, void* stream);
+                        int dx_accumulate, void* stream);
 /* x + f(LN(x)) (modules.py:293-294, 342-343): dx (f32) = dres + LN backward of dy, one pass
- * (x f32, dy f32 / bf16, cols % 8 == 0, 32-B aligned rows); dx16 as in comet_layernorm_bwd. */
+ * (x f32, dy f32 / bf16, cols % 8 == 0, 32-B aligned rows). */
 int comet_layernorm_bwd_res(int dtype_x, int dtype_dy, const void* x, const void* dy, const float* dres,
                             const float* mean, const float* rstd, const float* weight, float* dx,
-                            float* dweight, float* dbias, int64_t rows, int64_t cols, void* dx16, void* stream);
+                            float* dweight, float* dbias, int64_t rows, int64_t cols, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused multi-head attention forward (flash style: LDS-staged K/V, online softmax, MFMA for
