@@ -468,7 +468,8 @@ template <typename TO>
 __global__ void __launch_bounds__(256)
 tokens_wave4_kernel(const float* __restrict__ coords, const float* __restrict__ feats, int latent,
                     const float* __restrict__ corr, int64_t ldcorr, int corrdim,
-                    const float* __restrict__ pos, int tdim, TO* __restrict__ x, int64_t ldx, int64_t rows, int S) {
+                    const float* __restrict__ pos, int tdim, TO* __restrict__ x, int64_t ldx, int64_t rows, int S,
+                    int pairs) {
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= rows) return;
   const int lane = threadIdx.x & 63;
@@ -490,6 +491,22 @@ tokens_wave4_kernel(const float* __restrict__ coords, const float* __restrict__ 
       continue;
     }
     loadn<4>(prow + c0, v);
+    if (pairs && c0 < 2 * E && E % 2 == 0) {
+      // flow embedding: columns (2k, 2k + 1) are sin and cos of one argument (E and c0 even: a pair
+      // never straddles the x / y halves) -- one sincosf per pair, the values of sinf / cosf
+#pragma unroll
+      for (int e = 0; e < 4; e += 2) {
+        const int c = c0 + e;
+        const float a = c < E ? fx : fy;
+        const int cc = c < E ? c : c - E;
+        float sn, cs;
+        sincosf(a * ((float)cc * dscale), &sn, &cs);
+        v[e] += sn;
+        v[e + 1] += cs;
+      }
+      storen<4>(xrow + c0, v);
+      continue;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int c = c0 + e;
@@ -929,10 +946,11 @@ extern "C" int comet_tracker_tokens(int dtype_out, const float* coords, const fl
                                         "aligned x / pos");
   if (wave4 && (ldx != tdim || (getenv("COMET_TOKENS_ROWS") == nullptr && getenv("COMET_TOKENS_FLAT") == nullptr))) {
     const unsigned gr = (unsigned)cdiv(rows, 4);
+    const int pairs = getenv("COMET_TOKENS_NO_SINCOS") == nullptr;  // measurement: sinf / cosf per column
     if (dtype_out == COMET_F32)
-      hipLaunchKernelGGL((tokens_wave4_kernel<float>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (float*)x, ldx, rows, S);
+      hipLaunchKernelGGL((tokens_wave4_kernel<float>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (float*)x, ldx, rows, S, pairs);
     else
-      hipLaunchKernelGGL((tokens_wave4_kernel<__bf16>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (__bf16*)x, ldx, rows, S);
+      hipLaunchKernelGGL((tokens_wave4_kernel<__bf16>), dim3(gr), dim3(256), 0, s, coords, feats, latent, corr, ldcorr, corrdim, pos, tdim, (__bf16*)x, ldx, rows, S, pairs);
   } else if (rows < (1ll << 31) && S > 0 && getenv("COMET_TOKENS_FLAT") == nullptr) {
     const RowBlock rb = make_rowblock(rows, tdim);
     const unsigned gr = (unsigned)cdiv(rb.nrows, rb.RB);

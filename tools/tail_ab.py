@@ -32,7 +32,17 @@ def main():
     ffeat = torch.randn(65536, 32, device="cuda")
     fco = torch.rand(65536, 2, device="cuda") * 31
     fout = torch.empty(65536, 147, device="cuda")
+    B, N, S, lat, corrdim = 1, 4096, 16, 128, 405
+    tdim = 2 * (lat // 2) + 2 + corrdim + lat + 1  # 664, the coarse tracker
+    tco = torch.rand(B * N * S, 2, device="cuda") * 60
+    tfe = torch.randn(B * N * S, lat, device="cuda")
+    tcorr = torch.randn(B * N * S, corrdim, device="cuda")
+    tpos = torch.randn(B * N, tdim, device="cuda")
+    tx = torch.empty(B * N * S, (tdim + 63) // 64 * 64, device="cuda", dtype=torch.bfloat16)
     cases = {
+        "tracker_tokens coarse (65536 rows, 664 -> 704 bf16)": (
+            lambda: ops.tracker_tokens(tco, tfe, lat, tcorr, corrdim, tpos, tdim, tx, B * N * S, S),
+            65536 * (704 * 2 + corrdim * 4 + lat * 4)),
         "corr_sample fine (65536 rows, C 32, r 3, 3 levels)": (
             lambda: ops.corr_sample(fpyr, 3, ffeat, fco, fout, 0, 4096, 1, 16), 65536 * (147 * 4 + 32 * 4 + 8 + 3 * 100 * 64)),
         "layernorm f32 65536 x 32 (tracker GroupNorm(1, 32))": (
