@@ -201,7 +201,7 @@ resize_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, int c, int
 // c in {8, 16, 32, 64, 128, 256}); the odd last row of y (floor pooling drops it) is written after.
 // (workgroup body) y / pool of image ni from the staged input image `img` in LDS
 // (and, when pl != nullptr, a copy of the image's pool in LDS, [oh / 2][ow / 2][c], for a second level)
-template <typename TI, typename TO>
+template <typename TI, typename TO, bool NTS = false>
 __device__ __forceinline__ void resize_pool_body(const TI* img, TO* __restrict__ y, TO* __restrict__ pool, int64_t ni,
                                                  int c, int h, int w, int oh, int ow, TO* pl = nullptr) {
   const int cg8 = c / 8, ph = oh / 2, pw = ow / 2;
@@ -209,6 +209,10 @@ __device__ __forceinline__ void resize_pool_body(const TI* img, TO* __restrict__
   const int lane = threadIdx.x & 63;
   TO* yo = y + ni * oh * ow * c;
   TO* po = pool + ni * ph * pw * c;
+  auto put = [&](TO* p, const float (&o)[8]) {
+    if constexpr (NTS) store8_nt(p, o);
+    else store8(p, o);
+  };
   auto pixel = [&](int oy, int ox, int cg, float (&o)[8]) {
     int64_t y0, y1, x0, x1;
     float fy, fx;
@@ -234,8 +238,8 @@ __device__ __forceinline__ void resize_pool_body(const TI* img, TO* __restrict__
     if (live) {
       pixel(2 * py, ox, cg, a);
       pixel(2 * py + 1, ox, cg, cq);
-      store8(yo + ((int64_t)(2 * py) * ow + ox) * c + cg * 8, a);
-      store8(yo + ((int64_t)(2 * py + 1) * ow + ox) * c + cg * 8, cq);
+      put(yo + ((int64_t)(2 * py) * ow + ox) * c + cg * 8, a);
+      put(yo + ((int64_t)(2 * py + 1) * ow + ox) * c + cg * 8, cq);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {  // the values y holds
         a[e] = to_f32(from_f32<TO>(a[e]));
@@ -249,7 +253,7 @@ __device__ __forceinline__ void resize_pool_body(const TI* img, TO* __restrict__
       o[e] = (a[e] + b + cq[e] + d) * 0.25f;
     }
     if (live && (ox & 1) == 0 && ox / 2 < pw) {
-      store8(po + ((int64_t)py * pw + ox / 2) * c + cg * 8, o);
+      put(po + ((int64_t)py * pw + ox / 2) * c + cg * 8, o);
       if (pl != nullptr) store8(pl + (py * pw + ox / 2) * c + cg * 8, o);
     }
   }
@@ -258,12 +262,12 @@ __device__ __forceinline__ void resize_pool_body(const TI* img, TO* __restrict__
       const int ox = it / cg8, cg = it - ox * cg8;
       float o[8];
       pixel(oh - 1, ox, cg, o);
-      store8(yo + ((int64_t)(oh - 1) * ow + ox) * c + cg * 8, o);
+      put(yo + ((int64_t)(oh - 1) * ow + ox) * c + cg * 8, o);
     }
   }
 }
 
-template <typename TI, typename TO>
+template <typename TI, typename TO, bool NTS>
 __global__ void __launch_bounds__(256)
 resize_pool_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, TO* __restrict__ pool, int c, int h,
                              int w, int oh, int ow) {
@@ -273,7 +277,7 @@ resize_pool_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, TO* _
   const uint4* src = reinterpret_cast<const uint4*>(x + ni * h * w * c);
   for (int i = threadIdx.x; i < nvec; i += 256) img_lds[i] = src[i];
   __syncthreads();
-  resize_pool_body<TI, TO>(reinterpret_cast<const TI*>(img_lds), y, pool, ni, c, h, w, oh, ow);
+  resize_pool_body<TI, TO, NTS>(reinterpret_cast<const TI*>(img_lds), y, pool, ni, c, h, w, oh, ow);
 }
 
 // The fine ShallowEncoder's tail in one pass per patch (blocks.py:97-110 with refine_track's pool):
@@ -285,7 +289,7 @@ resize_pool_nhwc8_img_kernel(const TI* __restrict__ x, TO* __restrict__ y, TO* _
 // x2 and t stay in LDS (one image buffer, t written over x2): neither the [n, h, w, C] sums nor the
 // conv2 output reach HBM (two resize-add passes and one 16.7M-row GEMM per step fewer). bf16,
 // C = 16 x NT16 (one 32-deep k step per 32 input channels).
-template <int NT16>
+template <int NT16, bool NTS>
 __global__ void __launch_bounds__(256)
 conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restrict__ u1, int h1, int w1,
                            const __bf16* __restrict__ u2, int h2, int w2, const __bf16* __restrict__ wt,
@@ -388,7 +392,7 @@ conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restric
   }
   __syncthreads();
   __bf16* pl = pool2 != nullptr ? reinterpret_cast<__bf16*>(img_lds + nvec + n1 + n2) : nullptr;
-  resize_pool_body<__bf16, __bf16>(xs, y, pool, ni, C, h, w, oh, ow, pl);
+  resize_pool_body<__bf16, __bf16, NTS>(xs, y, pool, ni, C, h, w, oh, ow, pl);
   if (pool2 == nullptr) return;
   // the second pyramid level: avgpool2 of the pool, from its LDS copy (avgpool2_rows_kernel's order)
   __syncthreads();
@@ -405,7 +409,8 @@ conv1x1_resize_pool_kernel(const __bf16* __restrict__ x, const __bf16* __restric
     load8(r1 + C, d);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = (a[e] + bq[e] + cq[e] + d[e]) * 0.25f;
-    store8(qo + (int64_t)q * C + cg * 8, o);
+    if constexpr (NTS) store8_nt(qo + (int64_t)q * C + cg * 8, o);
+    else store8(qo + (int64_t)q * C + cg * 8, o);
   }
 }
 
@@ -489,6 +494,13 @@ extern "C" int comet_resize_bilinear(int dtype_in, int dtype_out, int nhwc, cons
   return COMET_OK;
 }
 
+// y / pool (/ pool2) of the resize + pool kernels written with streaming stores: write-once maps that no
+// later kernel finds in L2 (1 % faster, profiles/r06_nt); COMET_RSP_NT=0 turns them off (read per call)
+static bool rsp_streaming_stores() {
+  const char* e = std::getenv("COMET_RSP_NT");
+  return e == nullptr || e[0] != '0';
+}
+
 extern "C" int comet_resize_bilinear_pool_nhwc(int dtype_in, int dtype_out, const void* x, void* y, void* pool,
                                                int64_t n, int64_t c, int64_t h, int64_t w, int64_t oh, int64_t ow,
                                                void* stream) {
@@ -502,9 +514,14 @@ extern "C" int comet_resize_bilinear_pool_nhwc(int dtype_in, int dtype_out, cons
                   "an input image of at most 32 KiB");
   hipStream_t s = as_stream(stream);
   const size_t lds = (size_t)(h * w * c * esz);
-#define RSP(TI, TO)                                                                                          \
-  hipLaunchKernelGGL((resize_pool_nhwc8_img_kernel<TI, TO>), dim3((unsigned)n), dim3(256), lds, s, (const TI*)x, \
-                     (TO*)y, (TO*)pool, (int)c, (int)h, (int)w, (int)oh, (int)ow)
+  const bool nts = rsp_streaming_stores();
+#define RSP(TI, TO)                                                                                            \
+  if (nts)                                                                                                     \
+    hipLaunchKernelGGL((resize_pool_nhwc8_img_kernel<TI, TO, true>), dim3((unsigned)n), dim3(256), lds, s,     \
+                       (const TI*)x, (TO*)y, (TO*)pool, (int)c, (int)h, (int)w, (int)oh, (int)ow);             \
+  else                                                                                                         \
+    hipLaunchKernelGGL((resize_pool_nhwc8_img_kernel<TI, TO, false>), dim3((unsigned)n), dim3(256), lds, s,    \
+                       (const TI*)x, (TO*)y, (TO*)pool, (int)c, (int)h, (int)w, (int)oh, (int)ow)
   if (dtype_in == COMET_F32 && dtype_out == COMET_F32) RSP(float, float);
   else if (dtype_in == COMET_F32 && dtype_out == COMET_BF16) RSP(float, __bf16);
   else if (dtype_in == COMET_BF16 && dtype_out == COMET_BF16) RSP(__bf16, __bf16);
@@ -532,13 +549,16 @@ extern "C" int comet_conv1x1_resize_pool_nhwc(const void* x, const void* up1, in
                   "comet_conv1x1_resize_pool_nhwc: bad up-sampled input size");
   hipStream_t s = as_stream(stream);
   const size_t lds = (size_t)lds_b;
-#define C1P(NT)                                                                                                   \
-  hipLaunchKernelGGL((conv1x1_resize_pool_kernel<NT>), dim3((unsigned)n), dim3(256), lds, s, (const __bf16*)x,      \
+  const bool nts = rsp_streaming_stores();
+#define C1P(NT, NTS)                                                                                              \
+  hipLaunchKernelGGL((conv1x1_resize_pool_kernel<NT, NTS>), dim3((unsigned)n), dim3(256), lds, s, (const __bf16*)x, \
                      (const __bf16*)up1, (int)h1, (int)w1, (const __bf16*)up2, (int)h2, (int)w2,                     \
                      (const __bf16*)weight, bias, (__bf16*)y, (__bf16*)pool, (__bf16*)pool2, (int)h, (int)w, (int)oh, \
                      (int)ow)
-  if (c == 32) C1P(2);
-  else C1P(4);
+  if (c == 32 && nts) C1P(2, true);
+  else if (c == 32) C1P(2, false);
+  else if (nts) C1P(4, true);
+  else C1P(4, false);
 #undef C1P
   COMET_CHECK_LAUNCH("comet_conv1x1_resize_pool_nhwc");
   return COMET_OK;

@@ -96,6 +96,18 @@ __device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
   reinterpret_cast<float4*>(p)[0] = float4{v[0], v[1], v[2], v[3]};
   reinterpret_cast<float4*>(p)[1] = float4{v[4], v[5], v[6], v[7]};
 }
+// streaming (non-temporal) variants, for write-once outputs no later kernel of the step finds in L2
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+__device__ __forceinline__ void store8_nt(__bf16* p, const float (&v)[8]) {
+  u32x4 u;
+  u.x = pack_bf16x2(v[0], v[1]); u.y = pack_bf16x2(v[2], v[3]);
+  u.z = pack_bf16x2(v[4], v[5]); u.w = pack_bf16x2(v[6], v[7]);
+  __builtin_nontemporal_store(u, reinterpret_cast<u32x4*>(p));
+}
+__device__ __forceinline__ void store8_nt(float* p, const float (&v)[8]) {
+  __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, reinterpret_cast<f32x4*>(p));
+  __builtin_nontemporal_store(f32x4{v[4], v[5], v[6], v[7]}, reinterpret_cast<f32x4*>(p) + 1);
+}
 
 // 4-element variants (16 B of f32, 8 B of bf16)
 __device__ __forceinline__ void load4(const float* p, float (&v)[4]) {

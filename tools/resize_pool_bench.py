@@ -33,11 +33,17 @@ def main():
     sep = lambda: ops.avgpool2_nhwc(ops.resize_bilinear(x, 31, 31, nhwc=True))  # noqa: E731
     fused = lambda: ops.resize_bilinear_pool(x, 31, 31)  # noqa: E731
     tail = lambda: ops.conv1x1_resize_pool(x, w, b, 31, 31, up1=u1, up2=u2)  # noqa: E731
+    tail2 = lambda: ops.conv1x1_resize_pool(x, w, b, 31, 31, up1=u1, up2=u2, pool2=True)  # noqa: E731
     nbytes = (x.numel() + u1.numel() + u2.numel()) * 2 + 65536 * (31 * 31 + 15 * 15) * 32 * 2
+    nbytes2 = nbytes + 65536 * 7 * 7 * 32 * 2
     for rep in range(2):
-        uf, cl, a, f, t = timed(unfused), timed(clone), timed(sep), timed(fused), timed(tail)
-        print(f"unfused tail {uf - cl:7.1f} us (clone excluded) | resize + avgpool2 {a:7.1f} us | resize_pool {f:7.1f} us "
-              f"| conv1x1_resize_pool with both adds {t:7.1f} us ({nbytes / t / 1e6:.2f} TB/s algorithmic)", flush=True)
+        for nt in ("0", "1"):  # COMET_RSP_NT: streaming stores of y / pool / pool2
+            os.environ["COMET_RSP_NT"] = nt
+            uf, cl, a, f, t, t2 = timed(unfused), timed(clone), timed(sep), timed(fused), timed(tail), timed(tail2)
+            print(f"NT={nt} unfused tail {uf - cl:7.1f} us (clone excluded) | resize + avgpool2 {a:7.1f} us | "
+                  f"resize_pool {f:7.1f} us | conv1x1_resize_pool with both adds {t:7.1f} us "
+                  f"({nbytes / t / 1e6:.2f} TB/s algorithmic), + pool2 {t2:7.1f} us ({nbytes2 / t2 / 1e6:.2f} TB/s)",
+                  flush=True)
 
 
 if __name__ == "__main__":
